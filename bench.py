@@ -1,0 +1,247 @@
+"""Throughput bench: the RDUNet_T diffusion TRAIN STEP (BASELINE.json metric,
+config 2 at N=1: batch 16 per GPU, 256x256x3 synthetic sigma in {15,25,50},
+bf16 compute with fp32 master weights/accumulation).
+
+One step = t draw + interpolation + RDUNet_T(32) forward + Charbonnier loss +
+backward + global-norm clip (1.0) + fused AdamW update (lr 1e-4, wd 1e-4),
+i.e. train_step_checkpointed followed by optimizer.step() EVERY step (the
+reference steps every 4th batch; stepping every batch is strictly more work).
+For N>1 (torchrun, one process per GPU) each rank trains on its own 16 images
+and gradients are all-reduced over RCCL, bucketed and overlapped with the
+backward (weak scaling).
+
+Prints ONE JSON line (rank 0).  Extra objects:
+  roofline      dominant kernel instantiation, achieved algorithmic TFLOP/s or
+                GB/s measured with HIP events on the compute stream over the timed
+                region, against the MI355X peak (MI355X_MICROARCH.md)
+  cpu_baseline  the CPU oracle (torch fp32 NCHW, the reference's aten math) train
+                step at batch 2 on this host's cores, bounded sample
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+PEAK_BF16_TFLOPS = 2500.0   # dense MFMA (MI355X_MICROARCH.md chip table)
+PEAK_F32_TFLOPS = 157.3
+PEAK_HBM_GBS = 8000.0
+
+
+class EventTracer:
+    """engine.TRACER: HIP events around the launches of selected kernels."""
+
+    def __init__(self, keys=None):
+        self.keys = keys      # None = every traced launch
+        self.records = []     # (info, start, end)
+
+    def start(self, info):
+        if self.keys is not None and info[2] not in self.keys:
+            return None
+        s = torch.cuda.Event(enable_timing=True)
+        s.record()
+        return (info, s)
+
+    def stop(self, tok):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        self.records.append((tok[0], tok[1], e))
+
+    def summary(self):
+        torch.cuda.synchronize()
+        by = {}
+        for info, s, e in self.records:
+            ms = s.elapsed_time(e)
+            k = info[2]
+            d = by.setdefault(k, {"ms": 0.0, "n": 0, "flops": 0.0, "bytes": 0.0, "phases": set()})
+            d["ms"] += ms
+            d["n"] += 1
+            d["flops"] += info[3]
+            d["bytes"] += info[4]
+            d["phases"].add(info[0])
+        return by
+
+
+def cpu_baseline(seconds=12.0, batch=2, size=256):
+    """The CPU oracle's train step (fp32, torch aten on the host cores)."""
+    from oracle import rdunet_ref as R
+    from oracle.weights import make_params
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
+    torch.set_num_threads(threads)
+    params = {k: torch.from_numpy(v) for k, v in make_params(R.param_shapes(32), 0).items()}
+    g = torch.Generator().manual_seed(0)
+    clean = torch.rand(batch, 3, size, size, generator=g) * 2 - 1
+    noisy = clean + (25 / 255 * 2) * torch.randn(batch, 3, size, size, generator=g)
+    t = torch.randint(0, 21, (batch,), generator=g)
+    R.train_step(params, clean, noisy, t, 20)  # warm-up
+    n, t0 = 0, time.perf_counter()
+    while True:
+        R.train_step(params, clean, noisy, t, 20)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or n >= 50:
+            break
+    return {"value": round(batch * n / el, 4), "unit": "images/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"{n} oracle train steps (fwd+Charbonnier+bwd+clip) of RDUNet_T(32) fp32 at batch {batch} "
+                      f"x 3x{size}x{size}, {el:.1f}s on the host CPU"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=16, help="images per GPU")
+    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--base-filters", type=int, default=32)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--layer-report", default="", help="write a per-kernel time table (json) here")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import vub_image_denoising_amd as vm
+    from vub_image_denoising_amd import engine as E
+    from vub_image_denoising_amd.ddp import GradSync
+    from vub_image_denoising_amd.diffusion_RDUnet import DiffusionModel, train_step_device
+    from vub_image_denoising_amd.optim import FusedAdamW
+
+    torch.manual_seed(1234)
+    unet = vm.RDUNet_T(base_filters=args.base_filters).to(dev).set_compute_dtype(args.dtype)
+    model = DiffusionModel(unet, timesteps=20)
+    # synthetic data resident in HBM: one batch per sigma, rank-specific seed
+    gen = torch.Generator(device=dev).manual_seed(1234 + 7919 * rank)
+    batches = []
+    for sigma in (15.0, 25.0, 50.0):
+        clean = torch.rand(args.batch, 3, args.size, args.size, generator=gen, device=dev) * 2 - 1
+        noisy = clean + (sigma / 255.0 * 2.0) * torch.randn(args.batch, 3, args.size, args.size, generator=gen,
+                                                            device=dev)
+        batches.append((noisy, clean))
+    torch.manual_seed(99 + rank)  # t draws (torch.randint on the device)
+
+    opt = None
+
+    def step(i):
+        nonlocal opt
+        noisy, clean = batches[i % 3]
+        loss = train_step_device(model, clean, noisy, opt if opt is not None else _NoOpt(), "uniform", 1.0)
+        if opt is None:
+            return loss
+        opt.step()
+        return loss
+
+    class _NoOpt:
+        def zero_grad(self, set_to_none=True):
+            for p in model.parameters():
+                p.grad = None
+
+    step(0)  # builds the flat parameter buffer and the engine
+    fp = unet._rdn_flat
+    opt = FusedAdamW(model.parameters(), lr=1e-4, weight_decay=1e-4)
+    if world > 1:
+        fp.grad_sync = GradSync(fp, bucket_mb=25.0)
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+
+    # per-kernel profile pass (not timed): find the dominant kernel instantiation
+    prof = EventTracer()
+    E.TRACER = prof
+    step(0)
+    E.TRACER = None
+    table = prof.summary()
+    dom = max(table, key=lambda k: table[k]["ms"])
+    if rank == 0 and args.layer_report:
+        with open(args.layer_report, "w") as f:
+            json.dump({k: {kk: (sorted(vv) if isinstance(vv, set) else vv) for kk, vv in d.items()}
+                       for k, d in sorted(table.items(), key=lambda kv: -kv[1]["ms"])}, f, indent=1)
+
+    # timed region: events only around the dominant kernel's launches
+    live = EventTracer(keys={dom})
+    E.TRACER = live
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss = step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    E.TRACER = None
+    if world > 1:
+        tt = torch.tensor([el], device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = tt.item()
+    loss_v = loss.item()
+    d = live.summary()[dom]
+
+    if rank == 0:
+        images = args.batch * world * args.steps
+        avg_ms = d["ms"] / d["n"]
+        flops_per = d["flops"] / d["n"]
+        bytes_per = d["bytes"] / d["n"]
+        peak_mfma = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_F32_TFLOPS
+        t_mfma = flops_per / (peak_mfma * 1e12)
+        t_hbm = bytes_per / (PEAK_HBM_GBS * 1e9)
+        if t_mfma >= t_hbm:
+            roof = {"bound": "mfma", "achieved": round(flops_per / (avg_ms * 1e-3) / 1e12, 2), "peak": peak_mfma,
+                    "unit": "TFLOP/s"}
+        else:
+            roof = {"bound": "hbm", "achieved": round(bytes_per / (avg_ms * 1e-3) / 1e9, 1), "peak": PEAK_HBM_GBS,
+                    "unit": "GB/s"}
+        roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
+        roof["traffic"] = None
+        roof["kernel"] = dom
+        roof["avg_launch_us"] = round(avg_ms * 1e3, 2)
+        roof["launches_per_step"] = d["n"] // args.steps
+        roof["share_of_step"] = round(d["ms"] / (el * 1e3), 4)
+        cpu = None if args.no_cpu_baseline else cpu_baseline(args.cpu_seconds)
+        out = {
+            "metric": "images/sec (256x256x3) RDUNet diffusion train step",
+            "value": round(images / el, 2),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(el * 1e3 / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic (seeded U(-1,1) clean + Gaussian sigma in {15,25,50}/255*2, resident in HBM)",
+            "config": {"workload": "RDUNet_T(base_filters=%d) diffusion train step, fwd+Charbonnier+bwd+clip+AdamW"
+                                   % args.base_filters,
+                       "global_batch": args.batch * world, "per_gpu_batch": args.batch,
+                       "image": [3, args.size, args.size], "timesteps": 20,
+                       "parallelism": f"dp{world}", "optimizer_step": "every step",
+                       "final_loss": round(loss_v, 5)},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

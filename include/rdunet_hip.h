@@ -1,0 +1,183 @@
+/*
+ * rdunet_hip.h — C ABI of librdunet_hip.so, the MI355X (gfx950) kernels of the
+ * diffusion-RDUNet denoising hot path.
+ *
+ * Every entry point takes plain device pointers, element strides and sizes plus
+ * a hipStream_t (passed as void*), launches asynchronously on that stream and
+ * returns 0 on success or a negative RDN_E* code; rdn_last_error() returns a
+ * thread-local message for the last failure on the calling thread.  The library
+ * never allocates, frees or synchronises, so every call is hipGraph-capture safe.
+ * Caller-owned workspaces are sized by the *_workspace_size queries.
+ *
+ * Layouts: activations NHWC with an explicit pixel stride (elements between two
+ * pixels) and a channel offset, so a conv can read/write a channel slice of a
+ * dense-block buffer (this is how the reference's torch.cat disappears).
+ * Weights stay in the reference's OIHW (Conv2d) / IOHW (ConvTranspose2d) fp32
+ * layout in the state_dict and are packed per call site by rdn_pack_weights.
+ *
+ * Reference interfaces replaced (file:line under pierregab/VUB_Image_denoising):
+ *   rdn_conv_fwd      nn.Conv2d 3x3 p1 + nn.PReLU (+ residual add, + torch.cat)
+ *                     diffusion_denoising/Unet/Unet_model.py:48-55,60-67,72-89,35-43;
+ *                     nn.Conv2d k2 s2 + PReLU  Unet_model.py:26-30;
+ *                     nn.ConvTranspose2d k2 s2 + PReLU  Unet_model.py:36-42;
+ *                     and (with packed transposed weights) their input gradients
+ *                     (aten convolution_backward, grad_input).
+ *   rdn_conv_wgrad /  aten convolution_backward grad_weight for the same convs.
+ *   rdn_wgrad_reduce
+ *   rdn_prelu_bwd     aten _prelu_kernel_backward (dx, dalpha) + conv grad_bias.
+ *   rdn_interp        x = a*noisy + (1-a)*clean, diffusion_RDUnet.py:90-100, :33-36.
+ *   rdn_pack_input    torch.cat((inputs, t.expand(...)), 1), Unet_model.py:135-136.
+ *   rdn_charbonnier_fwd/bwd  charbonnier_loss/combined_loss, diffusion_RDUnet.py:57-65.
+ *   rdn_sqnorm / rdn_clip_scale  torch.nn.utils.clip_grad_norm_, diffusion_RDUnet.py:113.
+ *   rdn_adam_step     torch.optim.Adam / AdamW step, diffusion_RDUnet.py:264-268,127.
+ *   rdn_sampling_combine  the x_t update of improved_sampling, diffusion_RDUnet.py:45-49.
+ */
+#ifndef RDUNET_HIP_H
+#define RDUNET_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { RDN_OK = 0, RDN_E_ARG = -1, RDN_E_SHAPE = -2, RDN_E_LAUNCH = -3 };
+
+/* element type of activations / packed weights; master weights and weight
+   gradients are always fp32 */
+enum { RDN_F32 = 0, RDN_BF16 = 1 };
+
+/* how GEMM row m (a pixel of the row grid n,h,w) gathers its K = taps*cin inputs */
+enum {
+  RDN_G_CONV3 = 0, /* 3x3, stride 1, pad 1: src (y+ky-1, x+kx-1), taps 9     */
+  RDN_G_S2 = 1,    /* 2x2, stride 2: src (2y+dy, 2x+dx) of a 2h x 2w grid, taps 4 */
+  RDN_G_PIX = 2    /* 1 tap, src (y, x): a plain per-pixel GEMM                */
+};
+
+/* epilogue flags of rdn_conv_fwd, applied in this order */
+enum {
+  RDN_EPI_BIAS = 1,      /* v += bias[c]                                     */
+  RDN_EPI_STORE_PRE = 2, /* pre[pix, c] = v (PReLU input kept for backward)  */
+  RDN_EPI_PRELU = 4,     /* v = v > 0 ? v : alpha[c] * v                     */
+  RDN_EPI_RESID = 8,     /* v += res[pix, res_c0 + c] for c < res_climit     */
+  RDN_EPI_ACCUM = 16,    /* v += out[pix, out_c0 + c] (gradient accumulation) */
+  RDN_EPI_SCATTER2 = 32, /* column j = tap*cout + c lands on pixel (2y+dy, 2x+dx) */
+  RDN_EPI_OUT_NCHW = 64  /* write fp32 NCHW out_nchw (residual from res_nchw)  */
+};
+
+typedef struct rdn_conv_desc {
+  int32_t dtype, gather, flags;
+  int32_t n, h, w;       /* GEMM row grid: M = n*h*w                          */
+  int32_t hin, win;      /* source image size                                 */
+  int32_t cin;           /* channels per tap; K = taps*cin; multiple of 8     */
+  const void* x; int64_t x_ps; int32_t x_c0;
+  const void* wp; int32_t kp;  /* packed weights [rows >= ncols padded to 128][kp] */
+  int32_t ncols;         /* valid GEMM columns                                */
+  int32_t cout;          /* channels per output pixel (scatter: ncols/4)      */
+  const float* bias; const float* alpha;
+  void* out; int64_t out_ps; int32_t out_c0;
+  void* pre; int64_t pre_ps;
+  const void* res; int64_t res_ps; int32_t res_c0; int32_t res_climit;
+  float* out_nchw; const float* res_nchw;
+  int32_t bm, bn;        /* tile override, 0 = automatic                      */
+} rdn_conv_desc;
+
+/* Implicit-GEMM convolution (MFMA) with the fused epilogue above. */
+int rdn_conv_fwd(const rdn_conv_desc* d, void* stream);
+
+typedef struct rdn_wgrad_desc {
+  int32_t dtype, gather;   /* gather of the B operand: RDN_G_CONV3 or RDN_G_S2 */
+  int32_t n, h, w;         /* pixel grid of operand A (reduction length n*h*w) */
+  int32_t hin, win;        /* grid of operand B                                */
+  const void* a; int64_t a_ps; int32_t a_c0; int32_t mdim;  /* rows of dW (A channels; A
+                           buffer zero padded to a multiple of 8 channels)     */
+  const void* b; int64_t b_ps; int32_t b_c0; int32_t ndim;  /* per-tap columns, multiple of 8 */
+  float* ws;               /* [splits][mdim][taps*ndim] partial sums           */
+  int32_t splits;          /* 0 = automatic (see rdn_wgrad_splits)             */
+} rdn_wgrad_desc;
+
+/* dW[m][tap][nd] partials = sum over pixels p of A[p][m] * B[gather(p,tap)][nd] */
+int rdn_conv_wgrad(const rdn_wgrad_desc* d, void* stream);
+/* split count the automatic mode would use, and the workspace it needs (bytes) */
+int rdn_wgrad_splits(const rdn_wgrad_desc* d);
+int64_t rdn_wgrad_workspace_size(const rdn_wgrad_desc* d);
+/* grad[(m*ndim_real+nd)*taps+tap] (+)= sum_s ws[s][m][tap*ndim+nd] for nd < ndim_real:
+   the reference's OIHW (Conv2d) / IOHW (ConvTranspose2d) order */
+int rdn_wgrad_reduce(const float* ws, int32_t splits, int32_t mdim, int32_t ndim, int32_t ndim_real,
+                     int32_t taps, float* grad, int32_t accumulate, void* stream);
+
+/* PReLU backward (+ conv bias gradient) over a pixel grid of `pixels` pixels:
+   dyp[p, c] = dy[p, c] * (pre[p, c] > 0 ? 1 : alpha[c])   (c < C; 0 for C <= c < cpad)
+   dalpha[c] += sum_{pre<=0} pre*dy ; dbias[c] += sum dyp.
+   dy is NHWC (dy_ps, dy_c0) or, when dy_nchw != NULL, fp32 NCHW of the (n,h,w) grid. */
+int rdn_prelu_bwd(int32_t dtype, int64_t pixels, int32_t n, int32_t h, int32_t w, int32_t C, int32_t cpad,
+                  const void* dy, int64_t dy_ps, int32_t dy_c0, const float* dy_nchw,
+                  const void* pre, int64_t pre_ps, const float* alpha,
+                  void* dyp, float* dalpha, float* dbias, void* stream);
+
+/* x[b] = a_b*noisy[b] + (1-a_b)*clean[b], a_b = tnorm[b]; fp32 NCHW, `per` elements per image */
+int rdn_interp(const float* clean, const float* noisy, const float* tnorm, int32_t batch, int64_t per,
+               float* x, void* stream);
+
+/* NHWC input image [n,h,w,cpad]: channels 0..c-1 from fp32 NCHW x, channel c from t
+   (t[b*t_sb + y*t_sh + x*t_sw], strides may be 0 to broadcast) when has_t, rest 0 */
+int rdn_pack_input(int32_t dtype, const float* x, int32_t n, int32_t c, int32_t h, int32_t w,
+                   const float* t, int64_t t_sb, int64_t t_sh, int64_t t_sw, int32_t has_t,
+                   void* out, int32_t cpad, void* stream);
+
+/* fp32 OIHW/IOHW weight -> packed GEMM operand [rows_pad][kp] of `dtype`. */
+enum {
+  RDN_PACK_CONV_FWD = 0,  /* W[co][ci][ky][kx] -> P[co][tap*cin_p + ci]               */
+  RDN_PACK_CONV_DGRAD = 1,/* W[co][ci][ky][kx] -> P[ci][tap'*cout_p + co], tap' flipped */
+  RDN_PACK_GEMM_T = 2     /* W[a][b][dy][dx] (a = K side) -> P[tap*d1 + b][a]          */
+};
+/* CONV_FWD packs W[a][b][t] -> P[a][tap*pad1 + b] (pad1 >= d1, zero fill), which also
+   serves ConvTranspose2d's input gradient in conv-s2 form (a = ci, b = co).
+   CONV_DGRAD packs P[b][tap'*pad0 + a] with tap' the 180-degree rotated tap.
+   GEMM_T packs the per-pixel GEMM of ConvTranspose2d forward / Conv2d-s2 dgrad;
+   its K (= d0) is zero padded to pad0. */
+int rdn_pack_weights(int32_t mode, int32_t dtype, const float* w, int32_t d0, int32_t d1, int32_t kh, int32_t kw,
+                     int32_t pad0, int32_t pad1, void* out, int32_t rows_pad, int32_t kp, void* stream);
+
+/* Charbonnier (+MSE) over `count` fp32 elements.  ws >= rdn_reduce_workspace_size(count).
+   out[0] = mean(sqrt(d^2+eps^2)), out[1] = mean(d^2). */
+int64_t rdn_reduce_workspace_size(int64_t count);
+int rdn_charbonnier_fwd(const float* pred, const float* target, int64_t count, float eps,
+                        float* ws, float* out, void* stream);
+/* dpred = gout[0] * (wc * d/sqrt(d^2+eps^2) + wm * 2d) / count */
+int rdn_charbonnier_bwd(const float* pred, const float* target, int64_t count, float eps,
+                        float wc, float wm, const float* gout, float* dpred, void* stream);
+
+/* out[0] = sqrt(sum g^2) over a flat fp32 buffer; out[1] = min(max_norm/(out[0]+1e-6), 1) */
+int rdn_sqnorm(const float* g, int64_t count, float max_norm, float* ws, float* out, void* stream);
+/* g *= coef[0] (device scalar; no host sync) */
+int rdn_clip_scale(float* g, int64_t count, const float* coef, void* stream);
+
+/* torch.optim.Adam(W) step over flat fp32 buffers.  decoupled = 1 -> AdamW
+   (p *= 1 - lr*wd), 0 -> Adam L2 (g += wd*p).  bc1 = 1-beta1^t, bc2 = 1-beta2^t.
+   grad_scale multiplies g first (e.g. 1/world_size). */
+int rdn_adam_step(float* p, const float* g, float* m, float* v, int64_t count,
+                  float lr, float beta1, float beta2, float eps, float wd, int32_t decoupled,
+                  float bc1, float bc2, float grad_scale, void* stream);
+
+/* improved_sampling update: x = x - (c1*f1 + a*y) + (c2*f2 + ap*y), with c1 = 1-a and
+   c2 = 1-ap rounded on the host exactly as the reference's Python scalars are */
+int rdn_sampling_combine(float* x, const float* f1, const float* f2, const float* y, int64_t count,
+                         float c1, float a, float c2, float ap, void* stream);
+
+/* dense layout converters (fp32 NCHW <-> NHWC slice of `dtype`) */
+int rdn_nchw_to_nhwc(int32_t dtype, const float* src, int32_t n, int32_t c, int32_t h, int32_t w,
+                     void* dst, int64_t dst_ps, int32_t dst_c0, void* stream);
+int rdn_nhwc_to_nchw(int32_t dtype, const void* src, int64_t src_ps, int32_t src_c0,
+                     int32_t n, int32_t c, int32_t h, int32_t w, float* dst, int32_t accumulate, void* stream);
+
+/* fill a [pixels][cols] NHWC slice with zeros */
+int rdn_zero_slice(int32_t dtype, void* dst, int64_t pixels, int64_t ps, int32_t c0, int32_t cols, void* stream);
+
+const char* rdn_version(void);
+const char* rdn_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RDUNET_HIP_H */

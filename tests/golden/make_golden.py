@@ -93,6 +93,11 @@ def main():
     RDUNet_T = unet_mod.RDUNet_T
     out = {}
 
+    # (0) initial weights: torch.manual_seed(0); RDUNet_T(16) (reference RNG stream)
+    torch.manual_seed(0)
+    m0 = RDUNet_T(base_filters=16)
+    out["init16_sums"] = np.array([v.double().sum().item() for v in m0.state_dict().values()])
+
     # (1) RDUNet_T(F0=16) forward, 1x3x64x64, scalar t=0.35 (sampling form [1,1,1,1])
     torch.manual_seed(0)
     m = RDUNet_T(base_filters=16).eval()

@@ -1,0 +1,130 @@
+"""ctypes binding of ``librdunet_hip.so`` (the C ABI in ``include/rdunet_hip.h``).
+
+The library is built in-tree (``vub_image_denoising_amd/librdunet_hip.so``) by
+``vub_image_denoising_amd.build.build_library`` / ``__graft_entry__.build``.
+Nothing here falls back to another implementation: if the library is missing
+or a call fails, a ``RuntimeError`` is raised.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "librdunet_hip.so")
+
+RDN_F32, RDN_BF16 = 0, 1
+RDN_G_CONV3, RDN_G_S2, RDN_G_PIX = 0, 1, 2
+EPI_BIAS, EPI_STORE_PRE, EPI_PRELU, EPI_RESID, EPI_ACCUM, EPI_SCATTER2, EPI_OUT_NCHW = 1, 2, 4, 8, 16, 32, 64
+PACK_CONV_FWD, PACK_CONV_DGRAD, PACK_GEMM_T = 0, 1, 2
+
+_vp, _i32, _i64, _f32 = C.c_void_p, C.c_int32, C.c_int64, C.c_float
+
+
+class ConvDesc(C.Structure):
+    _fields_ = [
+        ("dtype", _i32), ("gather", _i32), ("flags", _i32),
+        ("n", _i32), ("h", _i32), ("w", _i32), ("hin", _i32), ("win", _i32), ("cin", _i32),
+        ("x", _vp), ("x_ps", _i64), ("x_c0", _i32),
+        ("wp", _vp), ("kp", _i32), ("ncols", _i32), ("cout", _i32),
+        ("bias", _vp), ("alpha", _vp),
+        ("out", _vp), ("out_ps", _i64), ("out_c0", _i32),
+        ("pre", _vp), ("pre_ps", _i64),
+        ("res", _vp), ("res_ps", _i64), ("res_c0", _i32), ("res_climit", _i32),
+        ("out_nchw", _vp), ("res_nchw", _vp),
+        ("bm", _i32), ("bn", _i32),
+    ]
+
+
+class WgradDesc(C.Structure):
+    _fields_ = [
+        ("dtype", _i32), ("gather", _i32), ("n", _i32), ("h", _i32), ("w", _i32), ("hin", _i32), ("win", _i32),
+        ("a", _vp), ("a_ps", _i64), ("a_c0", _i32), ("mdim", _i32),
+        ("b", _vp), ("b_ps", _i64), ("b_c0", _i32), ("ndim", _i32),
+        ("ws", _vp), ("splits", _i32),
+    ]
+
+
+# name -> (restype, argtypes); every symbol include/rdunet_hip.h declares
+SIGNATURES = {
+    "rdn_conv_fwd": (_i32, [C.POINTER(ConvDesc), _vp]),
+    "rdn_conv_wgrad": (_i32, [C.POINTER(WgradDesc), _vp]),
+    "rdn_wgrad_splits": (_i32, [C.POINTER(WgradDesc)]),
+    "rdn_wgrad_workspace_size": (_i64, [C.POINTER(WgradDesc)]),
+    "rdn_wgrad_reduce": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _vp, _i32, _vp]),
+    "rdn_prelu_bwd": (_i32, [_i32, _i64, _i32, _i32, _i32, _i32, _i32, _vp, _i64, _i32, _vp, _vp, _i64, _vp,
+                             _vp, _vp, _vp, _vp]),
+    "rdn_interp": (_i32, [_vp, _vp, _vp, _i32, _i64, _vp, _vp]),
+    "rdn_pack_input": (_i32, [_i32, _vp, _i32, _i32, _i32, _i32, _vp, _i64, _i64, _i64, _i32, _vp, _i32, _vp]),
+    "rdn_pack_weights": (_i32, [_i32, _i32, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _i32, _i32, _vp]),
+    "rdn_reduce_workspace_size": (_i64, [_i64]),
+    "rdn_charbonnier_fwd": (_i32, [_vp, _vp, _i64, _f32, _vp, _vp, _vp]),
+    "rdn_charbonnier_bwd": (_i32, [_vp, _vp, _i64, _f32, _f32, _f32, _vp, _vp, _vp]),
+    "rdn_sqnorm": (_i32, [_vp, _i64, _f32, _vp, _vp, _vp]),
+    "rdn_clip_scale": (_i32, [_vp, _i64, _vp, _vp]),
+    "rdn_adam_step": (_i32, [_vp, _vp, _vp, _vp, _i64, _f32, _f32, _f32, _f32, _f32, _i32, _f32, _f32, _f32, _vp]),
+    "rdn_sampling_combine": (_i32, [_vp, _vp, _vp, _vp, _i64, _f32, _f32, _f32, _f32, _vp]),
+    "rdn_nchw_to_nhwc": (_i32, [_i32, _vp, _i32, _i32, _i32, _i32, _vp, _i64, _i32, _vp]),
+    "rdn_nhwc_to_nchw": (_i32, [_i32, _vp, _i64, _i32, _i32, _i32, _i32, _i32, _vp, _i32, _vp]),
+    "rdn_zero_slice": (_i32, [_i32, _vp, _i64, _i64, _i32, _i32, _vp]),
+    "rdn_version": (C.c_char_p, []),
+    "rdn_last_error": (C.c_char_p, []),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load_library(path: str = LIB_PATH):
+    """Load and type the library (no GPU work).  Raises if it is missing."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise RuntimeError(
+                f"librdunet_hip.so not found at {path}: build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc --offload-arch=gfx950)")
+        lib = C.CDLL(path)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def lib():
+    return _lib if _lib is not None else load_library()
+
+
+def check(rc: int, what: str = ""):
+    if rc != 0:
+        msg = lib().rdn_last_error().decode(errors="replace")
+        raise RuntimeError(f"librdunet_hip {what} failed ({rc}): {msg}")
+
+
+def stream_ptr() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def dtype_code(dt: torch.dtype) -> int:
+    if dt == torch.float32:
+        return RDN_F32
+    if dt == torch.bfloat16:
+        return RDN_BF16
+    raise ValueError(f"unsupported activation dtype {dt}")
+
+
+def require_device(*tensors):
+    for t in tensors:
+        if t is not None and (not t.is_cuda):
+            raise RuntimeError("vub_image_denoising_amd runs on the ROCm GPU only (HIP kernels); got a CPU tensor. "
+                               "Move the model and inputs to 'cuda'.")

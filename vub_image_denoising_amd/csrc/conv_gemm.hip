@@ -1,0 +1,286 @@
+// Implicit-GEMM convolution for gfx950 (MFMA), NHWC activations.
+//
+//   out[m, j] = epilogue( sum_k A[m, k] * P[j, k] )
+//
+// GEMM row m is a pixel of the row grid (n, h, w); K = taps * cin with
+// k = tap * cin + ci, so every 16-byte unit a lane gathers (8 bf16 / 4 fp32
+// channels of one source pixel) is contiguous in NHWC memory.  The tap decides
+// the source pixel (RDN_G_CONV3: 3x3 pad 1; RDN_G_S2: 2x2 stride 2; RDN_G_PIX:
+// same pixel).  P is the packed weight operand [rows][kp] (k contiguous).
+//
+// One kernel serves the 3x3 convs of every block (Unet_model.py:48-49,60-61,
+// 72-75,35), the 2x2/s2 down-sampling conv (:26), the 2x2/s2 transposed conv
+// (:36, as a per-pixel GEMM with a depth-to-space scatter epilogue) and the
+// input gradients of all three (the same three shapes with repacked weights).
+//
+// Tiling: 256 threads = 4 waves; block tile BM x BN; K staged through LDS in
+// steps of 8 units (128 B per row), double buffered with a register prefetch
+// of the next stage.  bf16: v_mfma_f32_16x16x32_bf16, fp32: v_mfma_f32_16x16x4_f32
+// (exact fp32, the mode parity is checked in).
+#include "rdn_common.h"
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int U = 8;                 // 16-byte units per LDS row per stage
+constexpr int ROWB = U * 16 + 16;    // padded LDS row (bytes)
+
+template <int GATHER> struct Taps;
+template <> struct Taps<RDN_G_CONV3> { static constexpr int N = 9; };
+template <> struct Taps<RDN_G_S2> { static constexpr int N = 4; };
+template <> struct Taps<RDN_G_PIX> { static constexpr int N = 1; };
+
+template <typename T, int BM, int BN, int WMW, int GATHER>
+__global__ __launch_bounds__(NT) void conv_gemm_kernel(rdn_conv_desc d, FastDiv fd_w, FastDiv fd_hw) {
+  constexpr int VEC = TypeInfo<T>::VEC;
+  constexpr int SK = U * VEC;
+  constexpr int WNW = 4 / WMW;
+  constexpr int WTM = BM / WMW, WTN = BN / WNW;
+  constexpr int MT = WTM / 16, NTL = WTN / 16;
+  constexpr int A_UNITS = BM * U, B_UNITS = BN * U;
+  constexpr int A_IT = (A_UNITS + NT - 1) / NT, B_IT = (B_UNITS + NT - 1) / NT;
+  constexpr int TAPS = Taps<GATHER>::N;
+  static_assert(MT >= 1 && NTL >= 1, "tile");
+
+  __shared__ __attribute__((aligned(16))) unsigned char lds[2 * (BM + BN) * ROWB];
+#define ldsA(b) (lds + (b) * (BM * ROWB))
+#define ldsB(b) (lds + 2 * BM * ROWB + (b) * (BN * ROWB))
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WMW, wn = wave / WMW;
+  const int64_t M = (int64_t)d.n * d.h * d.w;
+  const int64_t m0 = (int64_t)blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+  const int ku = tid & (U - 1);
+  const T* __restrict__ X = (const T*)d.x;
+  const T* __restrict__ WP = (const T*)d.wp;
+
+  // ---- per-thread A rows (fixed over the K loop)
+  int a_y[A_IT], a_x[A_IT];
+  int64_t a_base[A_IT];
+  bool a_ok[A_IT];
+#pragma unroll
+  for (int r = 0; r < A_IT; ++r) {
+    const int u = tid + r * NT;
+    const int64_t m = m0 + (u >> 3);
+    a_ok[r] = (u < A_UNITS) && (m < M);
+    const uint32_t mm = a_ok[r] ? (uint32_t)m : 0u;
+    const uint32_t nimg = fdiv(mm, fd_hw);
+    const uint32_t rem = mm - nimg * (uint32_t)(d.h * d.w);
+    const uint32_t y = fdiv(rem, fd_w);
+    const uint32_t x = rem - y * (uint32_t)d.w;
+    a_y[r] = (int)y;
+    a_x[r] = (int)x;
+    if (GATHER == RDN_G_S2)
+      a_base[r] = (((int64_t)nimg * d.hin + 2 * y) * d.win + 2 * x) * d.x_ps + d.x_c0;
+    else
+      a_base[r] = (((int64_t)nimg * d.hin + y) * d.win + x) * d.x_ps + d.x_c0;
+  }
+
+  const int cin = d.cin;
+  const int ktot = TAPS * cin;
+  const int nst = (ktot + SK - 1) / SK;
+  int tap = (ku * VEC) / cin, ci = (ku * VEC) - tap * cin;
+
+  u32x4 ra[A_IT], rb[B_IT];
+
+  auto load_stage = [&](int s) {
+#pragma unroll
+    for (int r = 0; r < A_IT; ++r) {
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (a_ok[r] && tap < TAPS) {
+        int64_t off;
+        bool ok = true;
+        if (GATHER == RDN_G_CONV3) {
+          const int dy = tap / 3 - 1, dx = tap % 3 - 1;
+          const int ys = a_y[r] + dy, xs = a_x[r] + dx;
+          ok = (ys >= 0) && (ys < d.hin) && (xs >= 0) && (xs < d.win);
+          off = a_base[r] + ((int64_t)dy * d.win + dx) * d.x_ps + ci;
+        } else if (GATHER == RDN_G_S2) {
+          off = a_base[r] + ((int64_t)(tap >> 1) * d.win + (tap & 1)) * d.x_ps + ci;
+        } else {
+          off = a_base[r] + ci;
+        }
+        if (ok) v = *(const u32x4*)(X + off);
+      }
+      ra[r] = v;
+    }
+#pragma unroll
+    for (int r = 0; r < B_IT; ++r) {
+      const int u = tid + r * NT;
+      if (u < B_UNITS) rb[r] = *(const u32x4*)(WP + (int64_t)(n0 + (u >> 3)) * d.kp + (int64_t)s * SK + ku * VEC);
+    }
+    ci += SK;
+    while (ci >= cin) { ci -= cin; ++tap; }
+  };
+  auto store_stage = [&](int buf) {
+#pragma unroll
+    for (int r = 0; r < A_IT; ++r) {
+      const int u = tid + r * NT;
+      if (u < A_UNITS) *(u32x4*)(ldsA(buf) + (u >> 3) * ROWB + ku * 16) = ra[r];
+    }
+#pragma unroll
+    for (int r = 0; r < B_IT; ++r) {
+      const int u = tid + r * NT;
+      if (u < B_UNITS) *(u32x4*)(ldsB(buf) + (u >> 3) * ROWB + ku * 16) = rb[r];
+    }
+  };
+
+  f32x4 acc[MT][NTL];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NTL; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int frag_row = lane & 15, frag_k = (lane >> 4) * 16;
+
+  load_stage(0);
+  store_stage(0);
+  __syncthreads();
+  for (int s = 0; s < nst; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < nst) load_stage(s + 1);
+#pragma unroll
+    for (int ks = 0; ks < U / 4; ++ks) {
+      u32x4 af[MT], bfr[NTL];
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+        af[i] = *(const u32x4*)(ldsA(buf) + (wm * WTM + i * 16 + frag_row) * ROWB + ks * 64 + frag_k);
+#pragma unroll
+      for (int j = 0; j < NTL; ++j)
+        bfr[j] = *(const u32x4*)(ldsB(buf) + (wn * WTN + j * 16 + frag_row) * ROWB + ks * 64 + frag_k);
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NTL; ++j) {
+          if constexpr (sizeof(T) == 2) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[i]),
+                                                                __builtin_bit_cast(bf16x8, bfr[j]), acc[i][j], 0, 0, 0);
+          } else {
+            // whole-vector casts (see rdn_common.h: element bit casts miscompile)
+            const f32x4 a4 = __builtin_bit_cast(f32x4, af[i]);
+            const f32x4 b4 = __builtin_bit_cast(f32x4, bfr[j]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[e], b4[e], acc[i][j], 0, 0, 0);
+          }
+        }
+    }
+    if (s + 1 < nst) store_stage(buf ^ 1);
+    __syncthreads();
+  }
+
+#undef ldsA
+#undef ldsB
+  // ---- fused epilogue
+  const int flags = d.flags;
+  T* __restrict__ OUT = (T*)d.out;
+  T* __restrict__ PRE = (T*)d.pre;
+  const T* __restrict__ RES = (const T*)d.res;
+  const int H = d.h, W = d.w;
+#pragma unroll
+  for (int j = 0; j < NTL; ++j) {
+    const int col = n0 + wn * WTN + j * 16 + (lane & 15);
+    if (col >= d.ncols) continue;
+    int c = col, tp = 0;
+    if (flags & RDN_EPI_SCATTER2) { tp = col / d.cout; c = col - tp * d.cout; }
+    const float bias = (flags & RDN_EPI_BIAS) ? d.bias[c] : 0.f;
+    const float alpha = (flags & RDN_EPI_PRELU) ? d.alpha[c] : 0.f;
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int64_t m = m0 + wm * WTM + i * 16 + (lane >> 4) * 4 + e;
+        if (m >= M) continue;
+        float v = acc[i][j][e] + bias;
+        int64_t opix = m;
+        int nimg = 0, y = 0, x = 0, Ho = H, Wo = W;
+        if (flags & (RDN_EPI_SCATTER2 | RDN_EPI_OUT_NCHW)) {
+          nimg = (int)fdiv((uint32_t)m, fd_hw);
+          const int rem = (int)m - nimg * H * W;
+          y = (int)fdiv((uint32_t)rem, fd_w);
+          x = rem - y * W;
+          if (flags & RDN_EPI_SCATTER2) {
+            Ho = 2 * H; Wo = 2 * W;
+            y = 2 * y + (tp >> 1);
+            x = 2 * x + (tp & 1);
+            opix = ((int64_t)nimg * Ho + y) * Wo + x;
+          }
+        }
+        if (flags & RDN_EPI_STORE_PRE) PRE[opix * d.pre_ps + c] = from_f32<T>(v);
+        if (flags & RDN_EPI_PRELU) v = v > 0.f ? v : alpha * v;
+        if (flags & RDN_EPI_OUT_NCHW) {
+          const int64_t o = (((int64_t)nimg * d.cout + c) * Ho + y) * Wo + x;
+          if (flags & RDN_EPI_RESID) v += d.res_nchw[o];
+          if (flags & RDN_EPI_ACCUM) v += d.out_nchw[o];
+          d.out_nchw[o] = v;
+        } else {
+          if ((flags & RDN_EPI_RESID) && c < d.res_climit) v += to_f32(RES[opix * d.res_ps + d.res_c0 + c]);
+          T* op = OUT + opix * d.out_ps + d.out_c0 + c;
+          if (flags & RDN_EPI_ACCUM) v += to_f32(*op);
+          *op = from_f32<T>(v);
+        }
+      }
+    }
+  }
+}
+
+template <typename T, int BM, int BN, int WMW>
+int launch_gather(const rdn_conv_desc* d, hipStream_t st) {
+  const int64_t M = (int64_t)d->n * d->h * d->w;
+  dim3 grid((unsigned)((M + BM - 1) / BM), (unsigned)((d->ncols + BN - 1) / BN));
+  FastDiv fw = make_fastdiv((uint32_t)d->w), fhw = make_fastdiv((uint32_t)(d->h * d->w));
+  switch (d->gather) {
+    case RDN_G_CONV3: conv_gemm_kernel<T, BM, BN, WMW, RDN_G_CONV3><<<grid, NT, 0, st>>>(*d, fw, fhw); break;
+    case RDN_G_S2: conv_gemm_kernel<T, BM, BN, WMW, RDN_G_S2><<<grid, NT, 0, st>>>(*d, fw, fhw); break;
+    default: conv_gemm_kernel<T, BM, BN, WMW, RDN_G_PIX><<<grid, NT, 0, st>>>(*d, fw, fhw); break;
+  }
+  return rdn_check_launch("rdn_conv_fwd");
+}
+
+template <typename T>
+int launch_typed(const rdn_conv_desc* d, hipStream_t st) {
+  int bn = d->bn;
+  if (bn == 0) bn = d->ncols <= 16 ? 16 : d->ncols <= 32 ? 32 : d->ncols <= 64 ? 64 : 128;
+  switch (bn) {
+    case 16: return launch_gather<T, 128, 16, 4>(d, st);
+    case 32: return launch_gather<T, 128, 32, 4>(d, st);
+    case 64: return launch_gather<T, 128, 64, 2>(d, st);
+    case 128: return launch_gather<T, 128, 128, 2>(d, st);
+  }
+  rdn_set_error("rdn_conv_fwd: unsupported bn=%d", bn);
+  return RDN_E_ARG;
+}
+
+}  // namespace
+
+extern "C" int rdn_conv_fwd(const rdn_conv_desc* d, void* stream) {
+  if (!d || !d->x || !d->wp) { rdn_set_error("rdn_conv_fwd: null descriptor/pointer"); return RDN_E_ARG; }
+  const int vec = d->dtype == RDN_BF16 ? 8 : 4;
+  if (d->dtype != RDN_F32 && d->dtype != RDN_BF16) { rdn_set_error("rdn_conv_fwd: bad dtype %d", d->dtype); return RDN_E_ARG; }
+  if (d->gather < RDN_G_CONV3 || d->gather > RDN_G_PIX) { rdn_set_error("rdn_conv_fwd: bad gather %d", d->gather); return RDN_E_ARG; }
+  if (d->n <= 0 || d->h <= 0 || d->w <= 0 || d->cin <= 0 || d->ncols <= 0) {
+    rdn_set_error("rdn_conv_fwd: empty shape n=%d h=%d w=%d cin=%d ncols=%d", d->n, d->h, d->w, d->cin, d->ncols);
+    return RDN_E_SHAPE;
+  }
+  if (d->cin % 8 || d->x_ps % vec || d->x_c0 % vec || d->kp % 64 || ((uintptr_t)d->x & 15) || ((uintptr_t)d->wp & 15)) {
+    rdn_set_error("rdn_conv_fwd: alignment (cin=%d x_ps=%lld x_c0=%d kp=%d) must keep 16-byte units", d->cin,
+                  (long long)d->x_ps, d->x_c0, d->kp);
+    return RDN_E_SHAPE;
+  }
+  const int taps = d->gather == RDN_G_CONV3 ? 9 : d->gather == RDN_G_S2 ? 4 : 1;
+  if (taps * d->cin > d->kp) { rdn_set_error("rdn_conv_fwd: kp=%d < K=%d", d->kp, taps * d->cin); return RDN_E_SHAPE; }
+  if (d->gather == RDN_G_S2 && (d->hin != 2 * d->h || d->win != 2 * d->w)) { rdn_set_error("rdn_conv_fwd: s2 grid mismatch"); return RDN_E_SHAPE; }
+  if (d->gather != RDN_G_S2 && (d->hin != d->h || d->win != d->w)) { rdn_set_error("rdn_conv_fwd: grid mismatch"); return RDN_E_SHAPE; }
+  if ((int64_t)d->n * d->h * d->w >= (1ll << 31)) { rdn_set_error("rdn_conv_fwd: too many pixels"); return RDN_E_SHAPE; }
+  if ((d->flags & RDN_EPI_SCATTER2) && (d->cout * 4 != d->ncols)) { rdn_set_error("rdn_conv_fwd: scatter needs ncols=4*cout"); return RDN_E_SHAPE; }
+  if ((d->flags & RDN_EPI_OUT_NCHW) ? !d->out_nchw : !d->out) { rdn_set_error("rdn_conv_fwd: null output"); return RDN_E_ARG; }
+  if ((d->flags & RDN_EPI_BIAS) && !d->bias) { rdn_set_error("rdn_conv_fwd: null bias"); return RDN_E_ARG; }
+  if ((d->flags & RDN_EPI_PRELU) && !d->alpha) { rdn_set_error("rdn_conv_fwd: null alpha"); return RDN_E_ARG; }
+  if ((d->flags & RDN_EPI_STORE_PRE) && !d->pre) { rdn_set_error("rdn_conv_fwd: null pre"); return RDN_E_ARG; }
+  if ((d->flags & RDN_EPI_RESID) && !((d->flags & RDN_EPI_OUT_NCHW) ? (const void*)d->res_nchw : d->res)) {
+    rdn_set_error("rdn_conv_fwd: null residual"); return RDN_E_ARG;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  return d->dtype == RDN_BF16 ? launch_typed<bf16>(d, st) : launch_typed<float>(d, st);
+}

@@ -1,0 +1,286 @@
+// Weight gradient of the implicit-GEMM convolutions (gfx950, MFMA).
+//
+//   ws[s][m][tap*ndim + nd] = sum_{p in split s} A[p][m] * B[gather(p, tap)][nd]
+//
+// A = the per-pixel operand on the reduction grid (n, h, w): dYpre for Conv2d
+// (rows = output channels), the input X for ConvTranspose2d (rows = input
+// channels).  B = the gathered operand: X under the conv's taps (RDN_G_CONV3:
+// 3x3 pad 1 at the same resolution; RDN_G_S2: (2y+dy, 2x+dx) on the 2h x 2w
+// grid, which is both Conv2d k2 s2's input and ConvTranspose2d k2 s2's output
+// gradient).  The K dimension (pixels) is split over blockIdx.z; a second
+// kernel sums the splits in a fixed order (deterministic) and writes the
+// reference's OIHW / IOHW layout (aten convolution_backward grad_weight of
+// Unet_model.py:26,35-36,48-49,60-61,72-75).
+//
+// Pixels are staged into LDS as [pixel][channel] rows; MFMA operands need the
+// pixel (k) index contiguous per lane, so bf16 fragments come out of LDS with
+// the gfx950 transpose read ds_read_b64_tr_b16 and fp32 fragments with one
+// ds_read_b32 per lane (v_mfma_f32_16x16x4_f32 takes one k per lane group).
+#include "rdn_common.h"
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int KP = 32;  // pixels per stage
+
+template <typename T, int BM, int BN, int WMW, int GATHER>
+__global__ __launch_bounds__(NT) void wgrad_kernel(rdn_wgrad_desc d, FastDiv fd_w, FastDiv fd_hw, int pchunk) {
+  constexpr int VEC = TypeInfo<T>::VEC;
+  constexpr int ES = sizeof(T);
+  constexpr int WNW = 4 / WMW;
+  constexpr int WTM = BM / WMW, WTN = BN / WNW;
+  constexpr int MT = WTM / 16, NTL = WTN / 16;
+  constexpr int AG = BM / VEC, BG = BN / VEC;          // 16-B groups per LDS row
+  constexpr int A_UNITS = KP * AG, B_UNITS = KP * BG;
+  constexpr int A_IT = (A_UNITS + NT - 1) / NT, B_IT = (B_UNITS + NT - 1) / NT;
+  constexpr int ROWA = BM * ES + 16, ROWB = BN * ES + 16;
+  constexpr int TAPS = GATHER == RDN_G_CONV3 ? 9 : 4;
+  static_assert(NT % AG == 0 && NT % BG == 0, "group");
+
+  __shared__ __attribute__((aligned(16))) unsigned char lds[2 * KP * (ROWA + ROWB)];
+#define ldsA(b) (lds + (b) * (KP * ROWA))
+#define ldsB(b) (lds + 2 * KP * ROWA + (b) * (KP * ROWB))
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WMW, wn = wave / WMW;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int ncol = TAPS * d.ndim;
+  const int64_t P = (int64_t)d.n * d.h * d.w;
+  const int64_t pbeg = (int64_t)blockIdx.z * pchunk;
+  const int64_t pend = pbeg + pchunk < P ? pbeg + pchunk : P;
+  const T* __restrict__ A = (const T*)d.a;
+  const T* __restrict__ B = (const T*)d.b;
+
+  // fixed channel group per thread
+  const int ag = tid % AG, bg = tid % BG;
+  const int am = m0 + ag * VEC;
+  const bool a_col_ok = am < d.mdim;
+  const int bcol = n0 + bg * VEC;
+  const bool b_col_ok = bcol < ncol;
+  const int btap = b_col_ok ? bcol / d.ndim : 0;
+  const int bnd = bcol - btap * d.ndim;
+  int bdy, bdx;
+  if (GATHER == RDN_G_CONV3) { bdy = btap / 3 - 1; bdx = btap % 3 - 1; }
+  else { bdy = btap >> 1; bdx = btap & 1; }
+
+  u32x4 ra[A_IT], rb[B_IT];
+  auto load_stage = [&](int64_t pb) {
+#pragma unroll
+    for (int r = 0; r < A_IT; ++r) {
+      const int u = tid + r * NT;
+      const int64_t p = pb + u / AG;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (u < A_UNITS && a_col_ok && p < pend) v = *(const u32x4*)(A + p * d.a_ps + d.a_c0 + am);
+      ra[r] = v;
+    }
+#pragma unroll
+    for (int r = 0; r < B_IT; ++r) {
+      const int u = tid + r * NT;
+      const int64_t p = pb + u / BG;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (u < B_UNITS && b_col_ok && p < pend) {
+        const uint32_t nimg = fdiv((uint32_t)p, fd_hw);
+        const uint32_t rem = (uint32_t)p - nimg * (uint32_t)(d.h * d.w);
+        const int y = (int)fdiv(rem, fd_w);
+        const int x = (int)rem - y * d.w;
+        int ys, xs;
+        if (GATHER == RDN_G_CONV3) { ys = y + bdy; xs = x + bdx; }
+        else { ys = 2 * y + bdy; xs = 2 * x + bdx; }
+        if (ys >= 0 && ys < d.hin && xs >= 0 && xs < d.win)
+          v = *(const u32x4*)(B + (((int64_t)nimg * d.hin + ys) * d.win + xs) * d.b_ps + d.b_c0 + bnd);
+      }
+      rb[r] = v;
+    }
+  };
+  auto store_stage = [&](int buf) {
+#pragma unroll
+    for (int r = 0; r < A_IT; ++r) {
+      const int u = tid + r * NT;
+      if (u < A_UNITS) *(u32x4*)(ldsA(buf) + (u / AG) * ROWA + ag * 16) = ra[r];
+    }
+#pragma unroll
+    for (int r = 0; r < B_IT; ++r) {
+      const int u = tid + r * NT;
+      if (u < B_UNITS) *(u32x4*)(ldsB(buf) + (u / BG) * ROWB + bg * 16) = rb[r];
+    }
+  };
+
+  f32x4 acc[MT][NTL];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NTL; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nst = (int)((pend - pbeg + KP - 1) / KP);
+  const int g = lane >> 4, li = lane & 15;
+  if (nst > 0) {
+    load_stage(pbeg);
+    store_stage(0);
+  }
+  __syncthreads();
+  for (int s = 0; s < nst; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < nst) load_stage(pbeg + (int64_t)(s + 1) * KP);
+    if constexpr (ES == 2) {
+      // transpose reads: lane 16g+4q+p supplies row (8g+q [+4]) cols (4p..4p+3)
+      const int q = li >> 2, pp = li & 3;
+      bf16x8 af[MT], bfr[NTL];
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const unsigned char* base = ldsA(buf) + (8 * g + q) * ROWA + (wm * WTM + i * 16 + 4 * pp) * 2;
+        i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, base));
+        i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, base + 4 * ROWA));
+        af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int j = 0; j < NTL; ++j) {
+        const unsigned char* base = ldsB(buf) + (8 * g + q) * ROWB + (wn * WTN + j * 16 + 4 * pp) * 2;
+        i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, base));
+        i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, base + 4 * ROWB));
+        bfr[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NTL; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int e = 0; e < KP / 4; ++e) {
+        float af[MT], bfr[NTL];
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+          af[i] = *(const float*)(ldsA(buf) + (4 * e + g) * ROWA + (wm * WTM + i * 16 + li) * 4);
+#pragma unroll
+        for (int j = 0; j < NTL; ++j)
+          bfr[j] = *(const float*)(ldsB(buf) + (4 * e + g) * ROWB + (wn * WTN + j * 16 + li) * 4);
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+          for (int j = 0; j < NTL; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    if (s + 1 < nst) store_stage(buf ^ 1);
+    __syncthreads();
+  }
+
+#undef ldsA
+#undef ldsB
+  float* __restrict__ ws = d.ws + (int64_t)blockIdx.z * d.mdim * ncol;
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NTL; ++j) {
+      const int col = n0 + wn * WTN + j * 16 + li;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = m0 + wm * WTM + i * 16 + g * 4 + e;
+        if (m < d.mdim && col < ncol) ws[(int64_t)m * ncol + col] = acc[i][j][e];
+      }
+    }
+}
+
+__global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int mdim, int ndim, int ndim_real,
+                                    int taps, float* __restrict__ grad, int accumulate) {
+  const int ncol = taps * ndim;
+  const int64_t total = (int64_t)mdim * ndim_real * taps;
+  for (int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; o < total; o += (int64_t)gridDim.x * blockDim.x) {
+    const int tap = (int)(o % taps);
+    const int64_t r = o / taps;
+    const int nd = (int)(r % ndim_real);
+    const int m = (int)(r / ndim_real);
+    const int64_t src = (int64_t)m * ncol + (int64_t)tap * ndim + nd;
+    float s = 0.f;
+    for (int z = 0; z < splits; ++z) s += ws[(int64_t)z * mdim * ncol + src];
+    grad[o] = accumulate ? grad[o] + s : s;
+  }
+}
+
+struct Cfg { int bm, bn; };
+static Cfg pick(const rdn_wgrad_desc* d) {
+  const int taps = d->gather == RDN_G_CONV3 ? 9 : 4;
+  Cfg c;
+  c.bm = d->mdim <= 16 ? 16 : d->mdim <= 32 ? 32 : 64;
+  c.bn = taps * d->ndim <= 64 ? 64 : 128;
+  return c;
+}
+
+static int auto_splits(const rdn_wgrad_desc* d) {
+  if (d->splits > 0) return d->splits;
+  const Cfg c = pick(d);
+  const int taps = d->gather == RDN_G_CONV3 ? 9 : 4;
+  const int64_t tiles = (int64_t)((d->mdim + c.bm - 1) / c.bm) * ((taps * d->ndim + c.bn - 1) / c.bn);
+  const int64_t P = (int64_t)d->n * d->h * d->w;
+  int64_t s = (1024 + tiles - 1) / tiles;                 // ~4 blocks per CU
+  const int64_t maxs = (P + 255) / 256;                   // >= 256 pixels per split
+  if (s > maxs) s = maxs;
+  if (s < 1) s = 1;
+  return (int)s;
+}
+
+template <typename T, int BM, int BN, int WMW>
+static int launch_g(const rdn_wgrad_desc* d, hipStream_t st) {
+  const int taps = d->gather == RDN_G_CONV3 ? 9 : 4;
+  const int splits = auto_splits(d);
+  const int64_t P = (int64_t)d->n * d->h * d->w;
+  int64_t pchunk = (P + splits - 1) / splits;
+  pchunk = (pchunk + KP - 1) / KP * KP;
+  dim3 grid((d->mdim + BM - 1) / BM, (taps * d->ndim + BN - 1) / BN, splits);
+  FastDiv fw = make_fastdiv((uint32_t)d->w), fhw = make_fastdiv((uint32_t)(d->h * d->w));
+  if (d->gather == RDN_G_CONV3)
+    wgrad_kernel<T, BM, BN, WMW, RDN_G_CONV3><<<grid, NT, 0, st>>>(*d, fw, fhw, (int)pchunk);
+  else
+    wgrad_kernel<T, BM, BN, WMW, RDN_G_S2><<<grid, NT, 0, st>>>(*d, fw, fhw, (int)pchunk);
+  return rdn_check_launch("rdn_conv_wgrad");
+}
+
+template <typename T>
+static int launch_t(const rdn_wgrad_desc* d, hipStream_t st) {
+  const Cfg c = pick(d);
+  if (c.bm == 16) return c.bn == 64 ? launch_g<T, 16, 64, 1>(d, st) : launch_g<T, 16, 128, 1>(d, st);
+  if (c.bm == 32) return c.bn == 64 ? launch_g<T, 32, 64, 2>(d, st) : launch_g<T, 32, 128, 2>(d, st);
+  return c.bn == 64 ? launch_g<T, 64, 64, 2>(d, st) : launch_g<T, 64, 128, 2>(d, st);
+}
+
+}  // namespace
+
+extern "C" int rdn_wgrad_splits(const rdn_wgrad_desc* d) { return d ? auto_splits(d) : RDN_E_ARG; }
+
+extern "C" int64_t rdn_wgrad_workspace_size(const rdn_wgrad_desc* d) {
+  if (!d) return RDN_E_ARG;
+  const int taps = d->gather == RDN_G_CONV3 ? 9 : 4;
+  return (int64_t)auto_splits(d) * d->mdim * taps * d->ndim * (int64_t)sizeof(float);
+}
+
+extern "C" int rdn_conv_wgrad(const rdn_wgrad_desc* d, void* stream) {
+  if (!d || !d->a || !d->b || !d->ws) { rdn_set_error("rdn_conv_wgrad: null pointer"); return RDN_E_ARG; }
+  if (d->dtype != RDN_F32 && d->dtype != RDN_BF16) { rdn_set_error("rdn_conv_wgrad: bad dtype"); return RDN_E_ARG; }
+  if (d->gather != RDN_G_CONV3 && d->gather != RDN_G_S2) { rdn_set_error("rdn_conv_wgrad: bad gather"); return RDN_E_ARG; }
+  const int vec = d->dtype == RDN_BF16 ? 8 : 4;
+  if (d->n <= 0 || d->h <= 0 || d->w <= 0 || d->mdim <= 0 || d->ndim <= 0) { rdn_set_error("rdn_conv_wgrad: empty shape"); return RDN_E_SHAPE; }
+  if (d->ndim % 8 || d->a_ps % vec || d->a_c0 % vec || d->b_ps % vec || d->b_c0 % vec ||
+      ((uintptr_t)d->a & 15) || ((uintptr_t)d->b & 15)) {
+    rdn_set_error("rdn_conv_wgrad: alignment (ndim=%d a_ps=%lld a_c0=%d b_ps=%lld b_c0=%d)", d->ndim,
+                  (long long)d->a_ps, d->a_c0, (long long)d->b_ps, d->b_c0);
+    return RDN_E_SHAPE;
+  }
+  if (d->gather == RDN_G_S2 ? (d->hin != 2 * d->h || d->win != 2 * d->w) : (d->hin != d->h || d->win != d->w)) {
+    rdn_set_error("rdn_conv_wgrad: grid mismatch"); return RDN_E_SHAPE;
+  }
+  if ((int64_t)d->n * d->h * d->w >= (1ll << 31)) { rdn_set_error("rdn_conv_wgrad: too many pixels"); return RDN_E_SHAPE; }
+  hipStream_t st = (hipStream_t)stream;
+  return d->dtype == RDN_BF16 ? launch_t<bf16>(d, st) : launch_t<float>(d, st);
+}
+
+extern "C" int rdn_wgrad_reduce(const float* ws, int32_t splits, int32_t mdim, int32_t ndim, int32_t ndim_real,
+                                int32_t taps, float* grad, int32_t accumulate, void* stream) {
+  if (!ws || !grad || splits <= 0 || mdim <= 0 || ndim <= 0 || ndim_real <= 0 || ndim_real > ndim || taps <= 0) {
+    rdn_set_error("rdn_wgrad_reduce: bad arguments"); return RDN_E_ARG;
+  }
+  const int64_t total = (int64_t)mdim * ndim_real * taps;
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 4096) blocks = 4096;
+  wgrad_reduce_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(ws, splits, mdim, ndim, ndim_real, taps, grad, accumulate);
+  return rdn_check_launch("rdn_wgrad_reduce");
+}

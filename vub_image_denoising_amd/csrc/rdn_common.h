@@ -1,0 +1,84 @@
+// Shared device helpers for librdunet_hip (gfx950 / CDNA4, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/rdunet_hip.h"
+
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) short i16x4;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+typedef __bf16 bf16;
+
+#define RDN_LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
+
+template <typename T> struct TypeInfo;
+template <> struct TypeInfo<float> { static constexpr int VEC = 4; };
+template <> struct TypeInfo<bf16> { static constexpr int VEC = 8; };
+
+__device__ __forceinline__ float to_f32(float v) { return v; }
+__device__ __forceinline__ float to_f32(bf16 v) { return (float)v; }
+template <typename T> __device__ __forceinline__ T from_f32(float v);
+template <> __device__ __forceinline__ float from_f32<float>(float v) { return v; }
+template <> __device__ __forceinline__ bf16 from_f32<bf16>(float v) { return (bf16)v; }
+
+// 16-byte unit <-> floats
+template <typename T> struct Unit16;
+template <> struct Unit16<float> {
+  static constexpr int N = 4;
+  // NOTE: whole-vector bit casts only.  hipcc (ROCm 7.2) miscompiles
+  // __builtin_bit_cast(float, v[i]) on an ext_vector element: it returns v[0].
+  __device__ static void unpack(const u32x4& u, float* f) {
+    const f32x4 v = __builtin_bit_cast(f32x4, u);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) f[i] = v[i];
+  }
+  __device__ static u32x4 pack(const float* f) {
+    f32x4 v;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = f[i];
+    return __builtin_bit_cast(u32x4, v);
+  }
+};
+__device__ __forceinline__ float bf16lo(unsigned int w) { return __builtin_bit_cast(float, w << 16); }
+__device__ __forceinline__ float bf16hi(unsigned int w) { return __builtin_bit_cast(float, w & 0xffff0000u); }
+template <> struct Unit16<bf16> {
+  static constexpr int N = 8;
+  __device__ static void unpack(const u32x4& u, float* f) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { f[2 * i] = bf16lo(u[i]); f[2 * i + 1] = bf16hi(u[i]); }
+  }
+  __device__ static u32x4 pack(const float* f) {
+    u32x4 u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      unsigned short lo = __builtin_bit_cast(unsigned short, (bf16)f[2 * i]);
+      unsigned short hi = __builtin_bit_cast(unsigned short, (bf16)f[2 * i + 1]);
+      u[i] = (unsigned int)lo | ((unsigned int)hi << 16);
+    }
+    return u;
+  }
+};
+
+// Fast unsigned division by a runtime-invariant divisor (n < 2^31).
+struct FastDiv {
+  uint32_t d, m, s;
+};
+static inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  uint32_t s = 0;
+  while ((1ull << s) < d) ++s;
+  f.s = s;
+  f.m = (uint32_t)((((1ull << 32) * ((1ull << s) - d)) / d) + 1);
+  return f;
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  uint32_t t = __umulhi(n, f.m);
+  return (t + n) >> f.s;
+}
+
+// error plumbing (host)
+void rdn_set_error(const char* fmt, ...);
+int rdn_check_launch(const char* what);

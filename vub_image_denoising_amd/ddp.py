@@ -1,0 +1,132 @@
+"""Data-parallel gradient synchronisation over RCCL (torch.distributed "nccl"
+backend on ROCm), overlapped with the fused backward.
+
+The reference has no distributed code; this is the new
+capability of config 3.  Images are independent (no BatchNorm), so DP is exact:
+the all-reduced mean gradient equals the single-process gradient of the
+concatenated batch.
+
+Design for MI355X (xGMI point-to-point mesh):
+
+* the gradient lives in ONE flat fp32 buffer (``engine.FlatParams.gflat``),
+  laid out in module registration order (input block first), which is the
+  REVERSE of backward completion order;
+* it is cut into ~``bucket_mb`` buckets of contiguous parameter ranges; a bucket
+  is launched (``all_reduce``, sum) on a side stream as soon as the engine's
+  backward has finished the last layer whose gradients it holds, so RCCL rings
+  run on the links while the remaining layers' dgrad/wgrad run on the compute
+  stream;
+* the 1/world average is folded into one in-place scale after the last
+  bucket (so clip_grad_norm_ sees the mean gradient, as torch DDP would).
+
+No wrapper around the model: ``train_step_checkpointed`` calls
+``model.unet(...)`` directly (diffusion_RDUnet.py:106), which would bypass a DDP
+wrapper around DiffusionModel anyway.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+def plan_buckets(sizes, offsets, bucket_elems):
+    """Group parameters (given in flat order) into contiguous buckets, filling
+    from the END of the flat buffer (first gradients to complete).  Returns a
+    list of (lo, hi, first_param_index) with flat ranges [lo, hi)."""
+    n = len(sizes)
+    buckets = []
+    hi_idx = n
+    while hi_idx > 0:
+        lo_idx = hi_idx - 1
+        acc = sizes[lo_idx]
+        while lo_idx > 0 and acc + sizes[lo_idx - 1] <= bucket_elems:
+            lo_idx -= 1
+            acc += sizes[lo_idx]
+        lo = offsets[lo_idx]
+        hi = offsets[hi_idx] if hi_idx < n else None
+        buckets.append((lo, hi, lo_idx))
+        hi_idx = lo_idx
+    return buckets
+
+
+class GradSync:
+    """Bucketed, backward-overlapped gradient all-reduce for a FlatParams."""
+
+    def __init__(self, fp, bucket_mb: float = 25.0, group=None, overlap: bool = True):
+        self.fp = fp
+        self.group = group
+        self.world = dist.get_world_size(group)
+        sizes = [p.numel() for p in fp.params]
+        offs = list(fp.offsets)
+        raw = plan_buckets(sizes, offs, int(bucket_mb * 2 ** 20 / 4))
+        self.buckets = []
+        self.param_bucket = [0] * len(sizes)
+        hi_idx = len(sizes)
+        for b, (lo, hi, lo_idx) in enumerate(raw):
+            self.buckets.append((lo, fp.numel if hi is None else hi))
+            for i in range(lo_idx, hi_idx):
+                self.param_bucket[i] = b
+            hi_idx = lo_idx
+        self.counts = [self.param_bucket.count(b) for b in range(len(self.buckets))]
+        self.overlap = overlap and fp.gflat.is_cuda
+        self.stream = torch.cuda.Stream(device=fp.gflat.device) if self.overlap else None
+        self._works = []
+        self._remaining = list(self.counts)
+        self._launched = [False] * len(self.buckets)
+        self._inv = None
+
+    # --- engine hooks -------------------------------------------------
+    def begin(self):
+        self._works = []
+        self._remaining = list(self.counts)
+        self._launched = [False] * len(self.buckets)
+
+    def params_done(self, indices):
+        """The gradients of these parameter indices are final on the compute
+        stream; launch every bucket that just became complete.  Every rank runs
+        the same backward, so buckets are issued in the same order everywhere."""
+        for i in indices:
+            b = self.param_bucket[i]
+            self._remaining[b] -= 1
+            if self._remaining[b] == 0:
+                self._launch(b)
+
+    def _launch(self, b):
+        if self._launched[b]:
+            return
+        self._launched[b] = True
+        lo, hi = self.buckets[b]
+        view = self.fp.gflat[lo:hi]
+        if self.overlap:
+            self.stream.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(self.stream):
+                self._works.append(dist.all_reduce(view, group=self.group, async_op=True))
+        else:
+            self._works.append(dist.all_reduce(view, group=self.group, async_op=True))
+
+    def finish(self):
+        """Launch what is left (in bucket order), wait, and average."""
+        for b in range(len(self.buckets)):
+            self._launch(b)
+        for w in self._works:
+            w.wait()
+        if self.overlap:
+            torch.cuda.current_stream().wait_stream(self.stream)
+        self._works = []
+        if self.world > 1:
+            self._average()
+
+    def _average(self):
+        g = self.fp.gflat
+        if g.is_cuda:
+            from . import _hip as H
+            if self._inv is None:
+                self._inv = torch.full((1,), 1.0 / self.world, dtype=torch.float32, device=g.device)
+            H.check(H.lib().rdn_clip_scale(g.data_ptr(), g.numel(), self._inv.data_ptr(), H.stream_ptr()), "avg")
+        else:
+            g.mul_(1.0 / self.world)
+
+    def sync(self):
+        """Non-overlapped form: all buckets after backward."""
+        self.begin()
+        self.finish()

@@ -1,0 +1,75 @@
+"""Fused Adam / AdamW over the flat parameter buffer: one ``rdn_adam_step``
+launch per step instead of torch's per-tensor (foreach) kernels.
+
+Same update as ``torch.optim.Adam`` / ``AdamW`` (the optimizers of
+diffusion_RDUnet.py:264-268 and main_diffusion_RDUnet.py:230), same
+``param_groups`` (so LR schedulers work) and a ``state_dict`` in torch's
+per-parameter format (``step``, ``exp_avg``, ``exp_avg_sq``), whose moment
+tensors are views of the flat moment buffers.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _hip as H
+from .engine import find_flat
+
+
+class FusedAdam(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, decoupled=False,
+                 grad_scale=1.0):
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
+        super().__init__(params, defaults)
+        if len(self.param_groups) != 1:
+            raise ValueError("FusedAdam works on one parameter group (the fused network's flat buffer)")
+        self.decoupled = decoupled
+        self.grad_scale = grad_scale
+        self._fp = None
+        self._step = 0
+
+    def _bind(self):
+        params = self.param_groups[0]["params"]
+        fp = find_flat(params)
+        if fp is None:
+            raise RuntimeError("FusedAdam needs the parameters of one GPU RDUNet (run a forward/backward first); "
+                               "use torch.optim.Adam(W) otherwise")
+        if self._fp is not fp:
+            self._fp = fp
+            self._m = torch.zeros_like(fp.flat)
+            self._v = torch.zeros_like(fp.flat)
+            self._step = 0
+            self._steps = torch.zeros((), dtype=torch.float32)
+            for p, off in zip(fp.params, fp.offsets):
+                n = p.numel()
+                self.state[p] = {"step": self._steps, "exp_avg": self._m[off:off + n].view_as(p),
+                                 "exp_avg_sq": self._v[off:off + n].view_as(p)}
+        return fp
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        fp = self._bind()
+        g = self.param_groups[0]
+        self._step += 1
+        self._steps.fill_(self._step)
+        b1, b2 = g["betas"]
+        H.check(H.lib().rdn_adam_step(fp.flat.data_ptr(), fp.gflat.data_ptr(), self._m.data_ptr(), self._v.data_ptr(),
+                                      fp.numel, float(g["lr"]), float(b1), float(b2), float(g["eps"]),
+                                      float(g["weight_decay"]), 1 if self.decoupled else 0,
+                                      1.0 - b1 ** self._step, 1.0 - b2 ** self._step, float(self.grad_scale),
+                                      H.stream_ptr()), "adam_step")
+        fp.generation += 1  # weights changed behind torch's version counters: repack
+        return loss
+
+    def zero_grad(self, set_to_none: bool = True):
+        fp = self._fp or find_flat(self.param_groups[0]["params"])
+        if fp is not None and not set_to_none:
+            fp.gflat.zero_()
+            return
+        super().zero_grad(set_to_none=set_to_none)
+
+
+class FusedAdamW(FusedAdam):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, grad_scale=1.0):
+        super().__init__(params, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, decoupled=True,
+                         grad_scale=grad_scale)
