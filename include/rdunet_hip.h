@@ -113,7 +113,9 @@ int rdn_wgrad_reduce(const float* ws, int32_t splits, int32_t mdim, int32_t ndim
 int rdn_prelu_bwd(int32_t dtype, int64_t pixels, int32_t n, int32_t h, int32_t w, int32_t C, int32_t cpad,
                   const void* dy, int64_t dy_ps, int32_t dy_c0, const float* dy_nchw,
                   const void* pre, int64_t pre_ps, const float* alpha,
-                  void* dyp, float* dalpha, float* dbias, void* stream);
+                  void* dyp, float* dalpha, float* dbias, float* ws, void* stream);
+/* per-block channel partials (deterministic, no atomics): bytes of `ws` needed */
+int64_t rdn_prelu_bwd_workspace_size(int32_t dtype, int64_t pixels, int32_t C, int32_t cpad);
 
 /* x[b] = a_b*noisy[b] + (1-a_b)*clean[b], a_b = tnorm[b]; fp32 NCHW, `per` elements per image */
 int rdn_interp(const float* clean, const float* noisy, const float* tnorm, int32_t batch, int64_t per,
@@ -137,7 +139,21 @@ enum {
    GEMM_T packs the per-pixel GEMM of ConvTranspose2d forward / Conv2d-s2 dgrad;
    its K (= d0) is zero padded to pad0. */
 int rdn_pack_weights(int32_t mode, int32_t dtype, const float* w, int32_t d0, int32_t d1, int32_t kh, int32_t kw,
-                     int32_t pad0, int32_t pad1, void* out, int32_t rows_pad, int32_t kp, void* stream);
+                     int32_t pad0, int32_t pad1, void* out, int32_t rows_pad, int32_t kp, int32_t ck, void* stream);
+/* ck > 0 (CONV_FWD / CONV_DGRAD of a 3x3 conv): chunked K order for the halo kernel,
+   k = chunk*KC + tap*ck + ci, KC = roundup(9*ck, 128 B / elem size).  ck must be
+   rdn_conv3_chunk(K-side channels, dtype); rdn_conv3_packed_k gives the kp to use. */
+int rdn_conv3_chunk(int32_t cin, int32_t dtype);
+int rdn_conv3_packed_k(int32_t cin, int32_t dtype);
+/* output-channel tile the 3x3 kernel uses for `ncols` columns (16..128) */
+int rdn_conv3_pick_bn(int32_t ncols);
+
+/* Many packs in one launch: `items` is a DEVICE array of n rdn_pack_item. */
+typedef struct rdn_pack_item {
+  const float* w; void* out;
+  int32_t mode, d0, d1, kh, kw, pad0, pad1, rows_pad, kp, ck;
+} rdn_pack_item;
+int rdn_pack_weights_batched(const rdn_pack_item* items, int32_t n, int32_t dtype, void* stream);
 
 /* Charbonnier (+MSE) over `count` fp32 elements.  ws >= rdn_reduce_workspace_size(count).
    out[0] = mean(sqrt(d^2+eps^2)), out[1] = mean(d^2). */

@@ -30,11 +30,17 @@ def _nchw(buf, N, H_, W_, c0, c):
 
 
 def _pack(mode, w, d0, d1, kh, kw, pad0, pad1, rows, kp, dt):
+    """3x3 modes use the chunked K layout of the halo kernel (rdn_conv3_chunk)."""
+    ck = 0
+    if kh == 3 and mode in (H.PACK_CONV_FWD, H.PACK_CONV_DGRAD):
+        kside = pad1 if mode == H.PACK_CONV_FWD else pad0
+        ck = H.lib().rdn_conv3_chunk(kside, H.dtype_code(dt))
+        kp = H.lib().rdn_conv3_packed_k(kside, H.dtype_code(dt))
     rows = (rows + 127) // 128 * 128
     kp = (kp + 63) // 64 * 64
     out = torch.zeros(rows, kp, dtype=dt, device="cuda")
     H.check(H.lib().rdn_pack_weights(mode, H.dtype_code(dt), w.data_ptr(), d0, d1, kh, kw, pad0, pad1, out.data_ptr(),
-                                     rows, kp, H.stream_ptr()), "pack")
+                                     rows, kp, ck, H.stream_ptr()), "pack")
     return out
 
 
@@ -257,10 +263,12 @@ def test_prelu_bwd(dt, C_, cpad, nchw):
         dy_args = (dyb.data_ptr(), 80, 16, None)
         dyr = _nchw(dyb, N, Hh, Ww, 16, C_)
     dyp = torch.full((P, cpad), 7.0, dtype=dt, device="cuda")
-    da = torch.zeros(C_, device="cuda")
-    db = torch.zeros(C_, device="cuda")
+    da = torch.full((C_,), 0.5, device="cuda")   # accumulates into existing gradients
+    db = torch.full((C_,), -0.25, device="cuda")
+    ws = torch.zeros(H.lib().rdn_prelu_bwd_workspace_size(H.dtype_code(dt), P, C_, cpad) // 4, device="cuda")
     H.check(H.lib().rdn_prelu_bwd(H.dtype_code(dt), P, N, Hh, Ww, C_, cpad, *dy_args, pre.data_ptr(), cpad,
-                                  a.data_ptr(), dyp.data_ptr(), da.data_ptr(), db.data_ptr(), H.stream_ptr()))
+                                  a.data_ptr(), dyp.data_ptr(), da.data_ptr(), db.data_ptr(), ws.data_ptr(),
+                                  H.stream_ptr()))
     torch.cuda.synchronize()
     x = _nchw(pre, N, Hh, Ww, 0, C_).requires_grad_(True)
     ar = a.cpu().requires_grad_(True)
@@ -268,8 +276,8 @@ def test_prelu_bwd(dt, C_, cpad, nchw):
     y.backward(dyr)
     assert _rel(_nchw(dyp, N, Hh, Ww, 0, C_), x.grad) < _tol(dt)
     assert torch.all(dyp[:, C_:].float() == 0)
-    assert _rel(da, ar.grad) < _tol(dt)
-    assert _rel(db, x.grad.sum((0, 2, 3))) < _tol(dt)
+    assert _rel(da - 0.5, ar.grad) < _tol(dt)
+    assert _rel(db + 0.25, x.grad.sum((0, 2, 3))) < _tol(dt)
 
 
 def test_charbonnier_clip_adam_combine():

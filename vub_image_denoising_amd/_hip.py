@@ -48,6 +48,11 @@ class WgradDesc(C.Structure):
     ]
 
 
+class PackItem(C.Structure):
+    _fields_ = [("w", _vp), ("out", _vp), ("mode", _i32), ("d0", _i32), ("d1", _i32), ("kh", _i32), ("kw", _i32),
+                ("pad0", _i32), ("pad1", _i32), ("rows_pad", _i32), ("kp", _i32), ("ck", _i32)]
+
+
 # name -> (restype, argtypes); every symbol include/rdunet_hip.h declares
 SIGNATURES = {
     "rdn_conv_fwd": (_i32, [C.POINTER(ConvDesc), _vp]),
@@ -56,10 +61,15 @@ SIGNATURES = {
     "rdn_wgrad_workspace_size": (_i64, [C.POINTER(WgradDesc)]),
     "rdn_wgrad_reduce": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _vp, _i32, _vp]),
     "rdn_prelu_bwd": (_i32, [_i32, _i64, _i32, _i32, _i32, _i32, _i32, _vp, _i64, _i32, _vp, _vp, _i64, _vp,
-                             _vp, _vp, _vp, _vp]),
+                             _vp, _vp, _vp, _vp, _vp]),
+    "rdn_prelu_bwd_workspace_size": (_i64, [_i32, _i64, _i32, _i32]),
     "rdn_interp": (_i32, [_vp, _vp, _vp, _i32, _i64, _vp, _vp]),
     "rdn_pack_input": (_i32, [_i32, _vp, _i32, _i32, _i32, _i32, _vp, _i64, _i64, _i64, _i32, _vp, _i32, _vp]),
-    "rdn_pack_weights": (_i32, [_i32, _i32, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _i32, _i32, _vp]),
+    "rdn_pack_weights": (_i32, [_i32, _i32, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _i32, _i32, _i32, _vp]),
+    "rdn_pack_weights_batched": (_i32, [_vp, _i32, _i32, _vp]),
+    "rdn_conv3_chunk": (_i32, [_i32, _i32]),
+    "rdn_conv3_packed_k": (_i32, [_i32, _i32]),
+    "rdn_conv3_pick_bn": (_i32, [_i32]),
     "rdn_reduce_workspace_size": (_i64, [_i64]),
     "rdn_charbonnier_fwd": (_i32, [_vp, _vp, _i64, _f32, _vp, _vp, _vp]),
     "rdn_charbonnier_bwd": (_i32, [_vp, _vp, _i64, _f32, _f32, _f32, _vp, _vp, _vp]),

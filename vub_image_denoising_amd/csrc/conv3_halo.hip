@@ -1,0 +1,350 @@
+// 3x3 / pad 1 / stride 1 convolution as an implicit GEMM with an LDS-resident
+// input halo (gfx950, MFMA).  Serves every 3x3 conv of the network in forward
+// (Unet_model.py:48-49,60-61,72-75,35) and their input gradients (the same conv
+// over dYpre with 180-degree-rotated, transposed weights).
+//
+// Block = 256 threads (4 waves) = a TH x TW = 8 x 16 output-pixel tile of one
+// image x BN output channels.  The input channels are walked in chunks of CK:
+// a chunk's (TH+2) x (TW+2) halo tile is loaded ONCE into LDS and feeds all 9
+// taps (the generic gather re-reads every input pixel 9x through L2).  The
+// weights stream through a double-buffered LDS stage of 128 bytes per output
+// channel (one tap of 64 bf16 / 32 fp32 channels, or several taps of a smaller
+// chunk).  The next chunk's halo is prefetched into registers during the
+// current chunk's 9 taps.  The epilogue stages the fp32 tile through LDS so
+// every global store (PReLU input, output, residual read, accumulate read) is
+// a 16-byte NHWC vector.
+//
+// Packed weight layout (rdn_pack_weights with ck > 0):
+//   P[n][chunk*KC + tap*CK + ci],  KC = roundup(9*CK, SK),  SK = 128 B / elem.
+#include "rdn_common.h"
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int TH = 8, TW = 16, BM = TH * TW;
+constexpr int HW_ = (TH + 2) * (TW + 2);   // halo pixels
+constexpr int ROWB = 160;                  // B-stage row: 128 B + 32 B pad (conflict-free ds_read_b128)
+
+template <int CKB> struct HaloRow { static constexpr int V = CKB >= 64 ? CKB + 32 : CKB; };
+
+template <typename T, int BN, int WMW, int CK>
+__global__ __launch_bounds__(NT, 2) void conv3_halo_kernel(rdn_conv_desc d, int tiles_x, int tiles_y) {
+  constexpr int ES = sizeof(T);
+  constexpr int VEC = TypeInfo<T>::VEC;
+  constexpr int SK = 128 / ES;                       // k per stage
+  constexpr int CKB = CK * ES;                       // bytes per halo pixel row (data)
+  constexpr int HROW = HaloRow<CKB>::V;
+  constexpr int SPC = (9 * CK + SK - 1) / SK;        // stages per chunk
+  constexpr int KC = SPC * SK;
+  constexpr int WNW = 4 / WMW;
+  constexpr int WTM = BM / WMW, WTN = BN / WNW;
+  constexpr int MT = WTM / 16, NTL = WTN / 16;
+  constexpr int HU = CK / VEC;                       // 16-B units per halo pixel
+  constexpr int H_UNITS = HW_ * HU;
+  constexpr int H_IT = (H_UNITS + NT - 1) / NT;
+  constexpr int B_UNITS = BN * 8;
+  constexpr int B_IT = (B_UNITS + NT - 1) / NT;
+  constexpr int HALO_BYTES = HW_ * HROW;
+  constexpr int MAIN_BYTES = HALO_BYTES + 2 * BN * ROWB;
+  constexpr int CROW = BN * 4 + 16;                  // epilogue fp32 tile row
+  constexpr int EPI_BYTES = BM * CROW;
+  constexpr int LDS_BYTES = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
+  static_assert(MT >= 1 && NTL >= 1 && (CK % VEC) == 0, "tile");
+
+  __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
+  unsigned char* const halo = lds;
+#define ldsB(b) (lds + HALO_BYTES + (b) * (BN * ROWB))
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WMW, wn = wave / WMW;
+  const int r = lane & 15, g = lane >> 4;
+  int bt = blockIdx.x;
+  const int tx = bt % tiles_x; bt /= tiles_x;
+  const int ty = bt % tiles_y;
+  const int nimg = bt / tiles_y;
+  const int y0 = ty * TH, x0 = tx * TW;
+  const int n0 = blockIdx.y * BN;
+  const T* __restrict__ X = (const T*)d.x;
+  const T* __restrict__ WP = (const T*)d.wp;
+  const int H = d.h, W = d.w;
+  const int nch = d.cin / CK;
+  const int nst = nch * SPC;
+
+  // ---- halo loader: unit u -> (halo pixel, 16-B channel group)
+  u32x4 hreg[H_IT];
+  auto load_halo = [&](int c) {
+#pragma unroll
+    for (int it = 0; it < H_IT; ++it) {
+      const int u = tid + it * NT;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (u < H_UNITS) {
+        const int hp = u / HU, cu = u - hp * HU;
+        const int hy = hp / (TW + 2), hx = hp - hy * (TW + 2);
+        const int yy = y0 + hy - 1, xx = x0 + hx - 1;
+        if (yy >= 0 && yy < H && xx >= 0 && xx < W)
+          v = *(const u32x4*)(X + (((int64_t)nimg * H + yy) * W + xx) * d.x_ps + d.x_c0 + c * CK + cu * VEC);
+      }
+      hreg[it] = v;
+    }
+  };
+  auto store_halo = [&]() {
+#pragma unroll
+    for (int it = 0; it < H_IT; ++it) {
+      const int u = tid + it * NT;
+      if (u < H_UNITS) {
+        const int hp = u / HU, cu = u - hp * HU;
+        *(u32x4*)(halo + hp * HROW + cu * 16) = hreg[it];
+      }
+    }
+  };
+  // ---- weight stage loader: 8 units (128 B) per output channel
+  u32x4 breg[B_IT];
+  const int ku = tid & 7;
+  auto load_b = [&](int s) {
+    const int c = s / SPC, j = s - c * SPC;
+#pragma unroll
+    for (int it = 0; it < B_IT; ++it) {
+      const int u = tid + it * NT;
+      if (u < B_UNITS)
+        breg[it] = *(const u32x4*)(WP + (int64_t)(n0 + (u >> 3)) * d.kp + (int64_t)c * KC + j * SK + ku * VEC);
+    }
+  };
+  auto store_b = [&](int buf) {
+#pragma unroll
+    for (int it = 0; it < B_IT; ++it) {
+      const int u = tid + it * NT;
+      if (u < B_UNITS) *(u32x4*)(ldsB(buf) + (u >> 3) * ROWB + ku * 16) = breg[it];
+    }
+  };
+
+  f32x4 acc[MT][NTL];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int jn = 0; jn < NTL; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // tile-local pixel of m-tile i, lane row r: (py, px) = (wm*WTM/16 + i, r)
+  const int py0 = wm * (WTM / 16);
+
+  load_halo(0);
+  store_halo();
+  load_b(0);
+  store_b(0);
+  __syncthreads();
+
+  for (int s = 0; s < nst; ++s) {
+    const int c = s / SPC, j = s - c * SPC;
+    const bool last_of_chunk = (j == SPC - 1);
+    if (j == 0 && c + 1 < nch) load_halo(c + 1);
+    if (s + 1 < nst) load_b(s + 1);
+    const int buf = s & 1;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      // this lane group's first k within the chunk
+      const int k = j * SK + ks * (4 * VEC) + g * VEC;
+      int tap = k / CK;
+      const int ci = k - tap * CK;
+      tap = tap < 9 ? tap : 8;  // padded k: zero weights, finite operand
+      const int ky = tap / 3, kx = tap - 3 * ky;
+      u32x4 af[MT], bfr[NTL];
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+        af[i] = *(const u32x4*)(halo + ((py0 + i + ky) * (TW + 2) + (r + kx)) * HROW + ci * ES);
+#pragma unroll
+      for (int jn = 0; jn < NTL; ++jn)
+        bfr[jn] = *(const u32x4*)(ldsB(buf) + (wn * WTN + jn * 16 + r) * ROWB + ks * 64 + g * 16);
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int jn = 0; jn < NTL; ++jn) {
+          if constexpr (ES == 2) {
+            acc[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[i]),
+                                                                 __builtin_bit_cast(bf16x8, bfr[jn]), acc[i][jn], 0, 0, 0);
+          } else {
+            const f32x4 a4 = __builtin_bit_cast(f32x4, af[i]);
+            const f32x4 b4 = __builtin_bit_cast(f32x4, bfr[jn]);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              acc[i][jn] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[e], b4[e], acc[i][jn], 0, 0, 0);
+          }
+        }
+    }
+    if (s + 1 < nst) store_b(buf ^ 1);
+    __syncthreads();
+    if (last_of_chunk && c + 1 < nch) {
+      store_halo();
+      __syncthreads();
+    }
+  }
+#undef ldsB
+
+  // ---- epilogue: fp32 tile through LDS, then 16-byte NHWC stores
+  float* const Ct = (float*)lds;
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int jn = 0; jn < NTL; ++jn)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        Ct[((wm * WTM + i * 16 + g * 4 + e) * CROW) / 4 + wn * WTN + jn * 16 + r] = acc[i][jn][e];
+  __syncthreads();
+
+  const int flags = d.flags;
+  T* __restrict__ OUT = (T*)d.out;
+  T* __restrict__ PRE = (T*)d.pre;
+  const T* __restrict__ RES = (const T*)d.res;
+  constexpr int UPR = BN / VEC;         // 16-B units per tile row
+  constexpr int E_UNITS = BM * UPR;
+  for (int u = tid; u < E_UNITS; u += NT) {
+    const int p = u / UPR, cu = u - p * UPR;
+    const int yy = y0 + p / TW, xx = x0 + p % TW;
+    const int c = n0 + cu * VEC;
+    if (yy >= H || xx >= W || c >= d.ncols) continue;
+    const int64_t opix = ((int64_t)nimg * H + yy) * W + xx;
+    float v[VEC];
+    {
+      const float* src = Ct + (p * CROW) / 4 + cu * VEC;
+#pragma unroll
+      for (int q = 0; q < VEC; q += 4) {
+        const f32x4 t4 = *(const f32x4*)(src + q);
+        v[q] = t4[0]; v[q + 1] = t4[1]; v[q + 2] = t4[2]; v[q + 3] = t4[3];
+      }
+    }
+    const bool full = c + VEC <= d.ncols;
+    if (flags & RDN_EPI_BIAS) {
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) v[q] += (c + q < d.ncols) ? d.bias[c + q] : 0.f;
+    }
+    if (flags & RDN_EPI_STORE_PRE) {
+      T* pp = PRE + opix * d.pre_ps + c;
+      if (full) *(u32x4*)pp = Unit16<T>::pack(v);
+      else
+        for (int q = 0; q < VEC && c + q < d.ncols; ++q) pp[q] = from_f32<T>(v[q]);
+    }
+    if (flags & RDN_EPI_PRELU) {
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) {
+        const float a = (c + q < d.ncols) ? d.alpha[c + q] : 0.f;
+        v[q] = v[q] > 0.f ? v[q] : a * v[q];
+      }
+    }
+    if (flags & RDN_EPI_OUT_NCHW) {
+      for (int q = 0; q < VEC && c + q < d.ncols; ++q) {
+        const int64_t o = (((int64_t)nimg * d.cout + c + q) * H + yy) * W + xx;
+        float w = v[q];
+        if (flags & RDN_EPI_RESID) w += d.res_nchw[o];
+        if (flags & RDN_EPI_ACCUM) w += d.out_nchw[o];
+        d.out_nchw[o] = w;
+      }
+      continue;
+    }
+    if (flags & RDN_EPI_RESID) {
+      const T* rp = RES + opix * d.res_ps + d.res_c0 + c;
+      if (full && c + VEC <= d.res_climit) {
+        float rv[VEC];
+        Unit16<T>::unpack(*(const u32x4*)rp, rv);
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) v[q] += rv[q];
+      } else {
+        for (int q = 0; q < VEC; ++q)
+          if (c + q < d.res_climit && c + q < d.ncols) v[q] += to_f32(rp[q]);
+      }
+    }
+    T* op = OUT + opix * d.out_ps + d.out_c0 + c;
+    if (full) {
+      if (flags & RDN_EPI_ACCUM) {
+        float ov[VEC];
+        Unit16<T>::unpack(*(const u32x4*)op, ov);
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) v[q] += ov[q];
+      }
+      *(u32x4*)op = Unit16<T>::pack(v);
+    } else {
+      for (int q = 0; q < VEC && c + q < d.ncols; ++q) {
+        float w = v[q];
+        if (flags & RDN_EPI_ACCUM) w += to_f32(op[q]);
+        op[q] = from_f32<T>(w);
+      }
+    }
+  }
+}
+
+template <typename T, int BN, int WMW, int CK>
+int launch_h(const rdn_conv_desc* d, hipStream_t st) {
+  const int tiles_x = (d->w + TW - 1) / TW, tiles_y = (d->h + TH - 1) / TH;
+  dim3 grid((unsigned)(d->n * tiles_x * tiles_y), (unsigned)((d->ncols + BN - 1) / BN));
+  conv3_halo_kernel<T, BN, WMW, CK><<<grid, NT, 0, st>>>(*d, tiles_x, tiles_y);
+  return rdn_check_launch("rdn_conv_fwd(conv3)");
+}
+
+// BN choice: the candidate minimising padded columns ceil(ncols/BN)*BN, ties to the larger BN
+static int pick_bn(int ncols) {
+  static const int cands[] = {128, 96, 80, 64, 48, 32, 16};
+  int best = 128, waste = 1 << 30;
+  for (int b : cands) {
+    const int w = (ncols + b - 1) / b * b - ncols;
+    if (w < waste) { waste = w; best = b; }
+  }
+  return best;
+}
+
+template <typename T, int CK>
+int launch_bn(const rdn_conv_desc* d, hipStream_t st) {
+  const int bn = d->bn ? d->bn : pick_bn(d->ncols);
+  switch (bn) {
+    case 16: return launch_h<T, 16, 4, CK>(d, st);
+    case 32: return launch_h<T, 32, 4, CK>(d, st);
+    case 48: return launch_h<T, 48, 4, CK>(d, st);
+    case 64: return launch_h<T, 64, 2, CK>(d, st);
+    case 80: return launch_h<T, 80, 4, CK>(d, st);
+    case 96: return launch_h<T, 96, 4, CK>(d, st);
+    case 128: return launch_h<T, 128, 2, CK>(d, st);
+  }
+  rdn_set_error("rdn_conv_fwd(conv3): unsupported bn=%d", bn);
+  return RDN_E_ARG;
+}
+
+}  // namespace
+
+int rdn_conv3_chunk_impl(int cin, int dtype) {
+  const int cap = dtype == RDN_BF16 ? 64 : 32;
+  int ck = cap;
+  while (ck > 8 && (cin % ck)) ck >>= 1;
+  return (cin % ck) ? -1 : ck;
+}
+
+extern "C" int rdn_conv3_chunk(int32_t cin, int32_t dtype) { return rdn_conv3_chunk_impl(cin, dtype); }
+
+extern "C" int rdn_conv3_packed_k(int32_t cin, int32_t dtype) {
+  const int ck = rdn_conv3_chunk_impl(cin, dtype);
+  if (ck < 0) return RDN_E_SHAPE;
+  const int sk = dtype == RDN_BF16 ? 64 : 32;
+  const int kc = (9 * ck + sk - 1) / sk * sk;
+  const int kp = (cin / ck) * kc;
+  return (kp + 63) / 64 * 64;
+}
+
+extern "C" int rdn_conv3_pick_bn(int32_t ncols) { return pick_bn(ncols); }
+
+int rdn_conv3_launch(const rdn_conv_desc* d, hipStream_t st) {
+  const int ck = rdn_conv3_chunk_impl(d->cin, d->dtype);
+  if (ck < 0) { rdn_set_error("rdn_conv_fwd(conv3): cin=%d not a multiple of 8", d->cin); return RDN_E_SHAPE; }
+  if (d->kp < rdn_conv3_packed_k(d->cin, d->dtype)) {
+    rdn_set_error("rdn_conv_fwd(conv3): kp=%d < packed K %d (pack with ck=%d)", d->kp,
+                  rdn_conv3_packed_k(d->cin, d->dtype), ck);
+    return RDN_E_SHAPE;
+  }
+  if (d->dtype == RDN_BF16) {
+    switch (ck) {
+      case 64: return launch_bn<bf16, 64>(d, st);
+      case 32: return launch_bn<bf16, 32>(d, st);
+      case 16: return launch_bn<bf16, 16>(d, st);
+      default: return launch_bn<bf16, 8>(d, st);
+    }
+  }
+  switch (ck) {
+    case 32: return launch_bn<float, 32>(d, st);
+    case 16: return launch_bn<float, 16>(d, st);
+    default: return launch_bn<float, 8>(d, st);
+  }
+}

@@ -23,7 +23,7 @@ namespace {
 
 constexpr int NT = 256;
 constexpr int U = 8;                 // 16-byte units per LDS row per stage
-constexpr int ROWB = U * 16 + 16;    // padded LDS row (bytes)
+constexpr int ROWB = U * 16 + 32;    // padded LDS row: 160 B = 10 slots, conflict-free ds_read_b128
 
 template <int GATHER> struct Taps;
 template <> struct Taps<RDN_G_CONV3> { static constexpr int N = 9; };
@@ -282,5 +282,6 @@ extern "C" int rdn_conv_fwd(const rdn_conv_desc* d, void* stream) {
     rdn_set_error("rdn_conv_fwd: null residual"); return RDN_E_ARG;
   }
   hipStream_t st = (hipStream_t)stream;
+  if (d->gather == RDN_G_CONV3) return rdn_conv3_launch(d, st);  // LDS-halo kernel (conv3_halo.hip)
   return d->dtype == RDN_BF16 ? launch_typed<bf16>(d, st) : launch_typed<float>(d, st);
 }

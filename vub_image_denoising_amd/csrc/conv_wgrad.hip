@@ -181,19 +181,41 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(rdn_wgrad_desc d, FastDiv fd_
     }
 }
 
-__global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int mdim, int ndim, int ndim_real,
-                                    int taps, float* __restrict__ grad, int accumulate) {
+// Split reduction: block = CPB consecutive workspace columns x SL split lanes
+// (consecutive threads -> consecutive columns: coalesced slab reads); each
+// thread sums splits sl, sl+SL, ... and the SL partials are added in a fixed
+// order through LDS (deterministic).  The result goes to the reference layout
+// [m][nd][tap] (OIHW / IOHW).
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int mdim, int ndim,
+                                                           int ndim_real, int taps, float* __restrict__ grad,
+                                                           int accumulate, int sl_count) {
+  const int cpb = 256 / sl_count;
+  const int cc = threadIdx.x % cpb, sl = threadIdx.x / cpb;
   const int ncol = taps * ndim;
-  const int64_t total = (int64_t)mdim * ndim_real * taps;
-  for (int64_t o = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; o < total; o += (int64_t)gridDim.x * blockDim.x) {
-    const int tap = (int)(o % taps);
-    const int64_t r = o / taps;
-    const int nd = (int)(r % ndim_real);
-    const int m = (int)(r / ndim_real);
-    const int64_t src = (int64_t)m * ncol + (int64_t)tap * ndim + nd;
-    float s = 0.f;
-    for (int z = 0; z < splits; ++z) s += ws[(int64_t)z * mdim * ncol + src];
-    grad[o] = accumulate ? grad[o] + s : s;
+  const int64_t total = (int64_t)mdim * ncol;
+  const int64_t o = (int64_t)blockIdx.x * cpb + cc;
+  float s = 0.f;
+  if (o < total) {
+    int z = sl;
+    for (; z + 3 * sl_count < splits; z += 4 * sl_count) {
+      const float a0 = ws[(int64_t)z * total + o], a1 = ws[(int64_t)(z + sl_count) * total + o];
+      const float a2 = ws[(int64_t)(z + 2 * sl_count) * total + o], a3 = ws[(int64_t)(z + 3 * sl_count) * total + o];
+      s += (a0 + a1) + (a2 + a3);
+    }
+    for (; z < splits; z += sl_count) s += ws[(int64_t)z * total + o];
+  }
+  __shared__ float red[256];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (sl == 0 && o < total) {
+    for (int q = 1; q < sl_count; ++q) s += red[q * cpb + cc];
+    const int m = (int)(o / ncol);
+    const int col = (int)(o - (int64_t)m * ncol);
+    const int tap = col / ndim, nd = col - tap * ndim;
+    if (nd < ndim_real) {
+      const int64_t dst = ((int64_t)m * ndim_real + nd) * taps + tap;
+      grad[dst] = accumulate ? grad[dst] + s : s;
+    }
   }
 }
 
@@ -212,8 +234,8 @@ static int auto_splits(const rdn_wgrad_desc* d) {
   const int taps = d->gather == RDN_G_CONV3 ? 9 : 4;
   const int64_t tiles = (int64_t)((d->mdim + c.bm - 1) / c.bm) * ((taps * d->ndim + c.bn - 1) / c.bn);
   const int64_t P = (int64_t)d->n * d->h * d->w;
-  int64_t s = (1024 + tiles - 1) / tiles;                 // ~4 blocks per CU
-  const int64_t maxs = (P + 255) / 256;                   // >= 256 pixels per split
+  int64_t s = (512 + tiles - 1) / tiles;                  // ~2 blocks per CU
+  const int64_t maxs = (P + 1023) / 1024;                 // >= 1024 pixels per split
   if (s > maxs) s = maxs;
   if (s < 1) s = 1;
   return (int)s;
@@ -245,12 +267,15 @@ static int launch_t(const rdn_wgrad_desc* d, hipStream_t st) {
 
 }  // namespace
 
-extern "C" int rdn_wgrad_splits(const rdn_wgrad_desc* d) { return d ? auto_splits(d) : RDN_E_ARG; }
+extern "C" int rdn_wgrad_splits(const rdn_wgrad_desc* d) {
+  if (!d) return RDN_E_ARG;
+  return d->gather == RDN_G_CONV3 ? rdn_wgrad3_splits(d) : auto_splits(d);
+}
 
 extern "C" int64_t rdn_wgrad_workspace_size(const rdn_wgrad_desc* d) {
   if (!d) return RDN_E_ARG;
   const int taps = d->gather == RDN_G_CONV3 ? 9 : 4;
-  return (int64_t)auto_splits(d) * d->mdim * taps * d->ndim * (int64_t)sizeof(float);
+  return (int64_t)rdn_wgrad_splits(d) * d->mdim * taps * d->ndim * (int64_t)sizeof(float);
 }
 
 extern "C" int rdn_conv_wgrad(const rdn_wgrad_desc* d, void* stream) {
@@ -270,6 +295,7 @@ extern "C" int rdn_conv_wgrad(const rdn_wgrad_desc* d, void* stream) {
   }
   if ((int64_t)d->n * d->h * d->w >= (1ll << 31)) { rdn_set_error("rdn_conv_wgrad: too many pixels"); return RDN_E_SHAPE; }
   hipStream_t st = (hipStream_t)stream;
+  if (d->gather == RDN_G_CONV3) return rdn_wgrad3_launch(d, st);  // LDS-halo kernel (wgrad3_halo.hip)
   return d->dtype == RDN_BF16 ? launch_t<bf16>(d, st) : launch_t<float>(d, st);
 }
 
@@ -278,9 +304,13 @@ extern "C" int rdn_wgrad_reduce(const float* ws, int32_t splits, int32_t mdim, i
   if (!ws || !grad || splits <= 0 || mdim <= 0 || ndim <= 0 || ndim_real <= 0 || ndim_real > ndim || taps <= 0) {
     rdn_set_error("rdn_wgrad_reduce: bad arguments"); return RDN_E_ARG;
   }
-  const int64_t total = (int64_t)mdim * ndim_real * taps;
-  int blocks = (int)((total + 255) / 256);
-  if (blocks > 4096) blocks = 4096;
-  wgrad_reduce_kernel<<<blocks, 256, 0, (hipStream_t)stream>>>(ws, splits, mdim, ndim, ndim_real, taps, grad, accumulate);
+  const int64_t total = (int64_t)mdim * ndim * taps;
+  int sl = 1;
+  while (sl < 16 && sl < splits) sl <<= 1;
+  const int cpb = 256 / sl;
+  const int64_t blocks = (total + cpb - 1) / cpb;
+  if (blocks > 0x7fffffff) { rdn_set_error("rdn_wgrad_reduce: too large"); return RDN_E_SHAPE; }
+  wgrad_reduce_kernel<<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(ws, splits, mdim, ndim, ndim_real, taps, grad,
+                                                                         accumulate, sl);
   return rdn_check_launch("rdn_wgrad_reduce");
 }

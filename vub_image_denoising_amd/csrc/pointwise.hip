@@ -50,7 +50,7 @@ __global__ __launch_bounds__(256) void prelu_bwd_kernel(int64_t pixels, int H, i
                                                         const T* __restrict__ dy, int64_t dy_ps, int dy_c0,
                                                         const float* __restrict__ dy_nchw, const T* __restrict__ pre,
                                                         int64_t pre_ps, const float* __restrict__ alpha, T* __restrict__ dyp,
-                                                        float* __restrict__ dalpha, float* __restrict__ dbias) {
+                                                        float* __restrict__ part) {
   constexpr int VEC = TypeInfo<T>::VEC;
   const int G = cpad / VEC;                 // groups per pixel
   const int ppb = 256 / G;                  // pixels per block iteration
@@ -97,7 +97,9 @@ __global__ __launch_bounds__(256) void prelu_bwd_kernel(int64_t pixels, int H, i
       *(u32x4*)(dyp + p * cpad + grp * VEC) = Unit16<T>::pack(o);
     }
   }
-  // block reduction per channel: LDS [ppb][cpad] x 2
+  // block reduction per channel: LDS [ppb][cpad] x 2, then one partial per
+  // (block, channel) -- no atomics (one address per channel would serialise
+  // thousands of blocks); prelu_finalize_kernel sums the partials.
   __shared__ float red[2][256 * 8];
 #pragma unroll
   for (int k = 0; k < VEC; ++k) {
@@ -105,7 +107,6 @@ __global__ __launch_bounds__(256) void prelu_bwd_kernel(int64_t pixels, int H, i
     red[1][tid * VEC + k] = active ? sb[k] : 0.f;
   }
   __syncthreads();
-  // thread t < cpad sums channel t over the ppb pixel lanes
   for (int c = tid; c < C; c += 256) {
     const int gg = c / VEC, kk = c % VEC;
     float a = 0.f, b = 0.f;
@@ -113,8 +114,25 @@ __global__ __launch_bounds__(256) void prelu_bwd_kernel(int64_t pixels, int H, i
       a += red[0][(q * G + gg) * VEC + kk];
       b += red[1][(q * G + gg) * VEC + kk];
     }
-    if (dalpha) atomicAdd(dalpha + c, a);
-    if (dbias) atomicAdd(dbias + c, b);
+    part[(int64_t)blockIdx.x * 2 * C + c] = a;
+    part[(int64_t)blockIdx.x * 2 * C + C + c] = b;
+  }
+}
+
+// one block per (channel, {alpha, bias}): sum the per-block partials in a
+// fixed order and add into the fp32 gradient
+__global__ __launch_bounds__(256) void prelu_finalize_kernel(const float* __restrict__ part, int nblk, int C,
+                                                             float* __restrict__ dalpha, float* __restrict__ dbias) {
+  const int c = blockIdx.x % C, which = blockIdx.x / C;
+  float s = 0.f;
+  for (int b = threadIdx.x; b < nblk; b += 256) s += part[(int64_t)b * 2 * C + which * C + c];
+  __shared__ float sh[4];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float* dst = which ? dbias : dalpha;
+    if (dst) dst[c] += (sh[0] + sh[1]) + (sh[2] + sh[3]);
   }
 }
 
@@ -149,28 +167,55 @@ __global__ void pack_input_kernel(const float* __restrict__ x, int N, int C, int
 }
 
 // ------------------------------------------------------------------ weight packing
+__device__ __forceinline__ float pack_value(int mode, const float* __restrict__ w, int d0, int d1, int kh, int kw,
+                                            int pad0, int pad1, int kc, int ck, int r, int k) {
+  const int taps = kh * kw;
+  if (mode == RDN_PACK_CONV_FWD) {  // P[a][tap*pad1 + b] = W[a][b][tap]  (chunked when ck > 0)
+    int tap, b;
+    if (ck > 0) { const int ch = k / kc, rem = k - ch * kc; tap = rem / ck; b = ch * ck + (rem - tap * ck); }
+    else { tap = k / pad1; b = k - tap * pad1; }
+    const int a = r;
+    if (a < d0 && b < d1 && tap < taps) return w[((int64_t)a * d1 + b) * taps + tap];
+  } else if (mode == RDN_PACK_CONV_DGRAD) {  // P[b][tap'*pad0 + a] = W[a][b][flip(tap')]
+    int tp, a;
+    if (ck > 0) { const int ch = k / kc, rem = k - ch * kc; tp = rem / ck; a = ch * ck + (rem - tp * ck); }
+    else { tp = k / pad0; a = k - tp * pad0; }
+    const int b = r;
+    if (a < d0 && b < d1 && tp < taps) {
+      const int ky = kh - 1 - tp / kw, kx = kw - 1 - tp % kw;
+      return w[((int64_t)a * d1 + b) * taps + ky * kw + kx];
+    }
+  } else {  // GEMM_T: P[tap*d1 + b][a] = W[a][b][tap], K = pad0 >= d0
+    const int tap = r / d1, b = r - tap * d1, a = k;
+    if (tap < taps && a < d0) return w[((int64_t)a * d1 + b) * taps + tap];
+  }
+  return 0.f;
+}
+
+static inline int chunk_kc(int ck, int dtype) {
+  const int sk = dtype == RDN_BF16 ? 64 : 32;
+  return ck > 0 ? (9 * ck + sk - 1) / sk * sk : 0;
+}
+
 template <typename T>
 __global__ void pack_weights_kernel(int mode, const float* __restrict__ w, int d0, int d1, int kh, int kw, int pad0,
-                                    int pad1, T* __restrict__ out, int rows_pad, int kp) {
-  const int taps = kh * kw;
+                                    int pad1, T* __restrict__ out, int rows_pad, int kp, int ck, int kc) {
   const int64_t total = (int64_t)rows_pad * kp;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int r = (int)(i / kp), k = (int)(i - (int64_t)r * kp);
-    float v = 0.f;
-    if (mode == RDN_PACK_CONV_FWD) {  // P[a][tap*pad1 + b] = W[a][b][tap]
-      const int tap = k / pad1, b = k - tap * pad1, a = r;
-      if (a < d0 && b < d1 && tap < taps) v = w[((int64_t)a * d1 + b) * taps + tap];
-    } else if (mode == RDN_PACK_CONV_DGRAD) {  // P[b][tap'*pad0 + a] = W[a][b][flip(tap')]
-      const int tp = k / pad0, a = k - tp * pad0, b = r;
-      if (a < d0 && b < d1 && tp < taps) {
-        const int ky = kh - 1 - tp / kw, kx = kw - 1 - tp % kw;
-        v = w[((int64_t)a * d1 + b) * taps + ky * kw + kx];
-      }
-    } else {  // GEMM_T: P[tap*d1 + b][a] = W[a][b][tap], K = pad0 >= d0
-      const int tap = r / d1, b = r - tap * d1, a = k;
-      if (tap < taps && a < d0) v = w[((int64_t)a * d1 + b) * taps + tap];
-    }
-    out[i] = from_f32<T>(v);
+    out[i] = from_f32<T>(pack_value(mode, w, d0, d1, kh, kw, pad0, pad1, kc, ck, r, k));
+  }
+}
+
+template <typename T>
+__global__ void pack_weights_batched_kernel(const rdn_pack_item* __restrict__ items, int sk) {
+  const rdn_pack_item it = items[blockIdx.y];
+  const int kc = it.ck > 0 ? (9 * it.ck + sk - 1) / sk * sk : 0;
+  const int64_t total = (int64_t)it.rows_pad * it.kp;
+  T* __restrict__ out = (T*)it.out;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(i / it.kp), k = (int)(i - (int64_t)r * it.kp);
+    out[i] = from_f32<T>(pack_value(it.mode, it.w, it.d0, it.d1, it.kh, it.kw, it.pad0, it.pad1, kc, it.ck, r, k));
   }
 }
 
@@ -335,23 +380,34 @@ __global__ void zero_slice_kernel(T* __restrict__ d, int64_t pixels, int64_t ps,
 // ================================================================== C ABI
 #define RDN_STREAM ((hipStream_t)stream)
 
+static int prelu_blocks(int dtype, int64_t pixels, int cpad) {
+  const int vec = dtype == RDN_BF16 ? 8 : 4;
+  const int G = cpad / vec, ppb = 256 / G;
+  return grid_for(pixels, ppb * 8, 1024);
+}
+
+extern "C" int64_t rdn_prelu_bwd_workspace_size(int32_t dtype, int64_t pixels, int32_t C, int32_t cpad) {
+  return (int64_t)prelu_blocks(dtype, pixels, cpad) * 2 * C * (int64_t)sizeof(float);
+}
+
 extern "C" int rdn_prelu_bwd(int32_t dtype, int64_t pixels, int32_t n, int32_t h, int32_t w, int32_t C, int32_t cpad,
                              const void* dy, int64_t dy_ps, int32_t dy_c0, const float* dy_nchw, const void* pre,
-                             int64_t pre_ps, const float* alpha, void* dyp, float* dalpha, float* dbias, void* stream) {
+                             int64_t pre_ps, const float* alpha, void* dyp, float* dalpha, float* dbias, float* ws,
+                             void* stream) {
   const int vec = dtype == RDN_BF16 ? 8 : 4;
-  if ((!dy && !dy_nchw) || !pre || !alpha || !dyp) { rdn_set_error("rdn_prelu_bwd: null pointer"); return RDN_E_ARG; }
+  if ((!dy && !dy_nchw) || !pre || !alpha || !dyp || !ws) { rdn_set_error("rdn_prelu_bwd: null pointer"); return RDN_E_ARG; }
   if (C <= 0 || cpad < C || cpad % vec || cpad / vec > 256 || pre_ps % vec || pixels != (int64_t)n * h * w) {
     rdn_set_error("rdn_prelu_bwd: bad shape C=%d cpad=%d pre_ps=%lld", C, cpad, (long long)pre_ps);
     return RDN_E_SHAPE;
   }
-  const int G = cpad / vec, ppb = 256 / G;
-  const int blocks = grid_for(pixels, ppb * 4, 2048);
+  const int blocks = prelu_blocks(dtype, pixels, cpad);
   if (dtype == RDN_BF16)
     prelu_bwd_kernel<bf16><<<blocks, 256, 0, RDN_STREAM>>>(pixels, h, w, C, cpad, (const bf16*)dy, dy_ps, dy_c0, dy_nchw,
-                                                          (const bf16*)pre, pre_ps, alpha, (bf16*)dyp, dalpha, dbias);
+                                                          (const bf16*)pre, pre_ps, alpha, (bf16*)dyp, ws);
   else
     prelu_bwd_kernel<float><<<blocks, 256, 0, RDN_STREAM>>>(pixels, h, w, C, cpad, (const float*)dy, dy_ps, dy_c0, dy_nchw,
-                                                           (const float*)pre, pre_ps, alpha, (float*)dyp, dalpha, dbias);
+                                                           (const float*)pre, pre_ps, alpha, (float*)dyp, ws);
+  if (dalpha || dbias) prelu_finalize_kernel<<<2 * C, 256, 0, RDN_STREAM>>>(ws, blocks, C, dalpha, dbias);
   return rdn_check_launch("rdn_prelu_bwd");
 }
 
@@ -376,12 +432,27 @@ extern "C" int rdn_pack_input(int32_t dtype, const float* x, int32_t n, int32_t 
   return rdn_check_launch("rdn_pack_input");
 }
 
+extern "C" int rdn_pack_weights_batched(const rdn_pack_item* items, int32_t n, int32_t dtype, void* stream) {
+  if (!items || n <= 0 || n > 65535) { rdn_set_error("rdn_pack_weights_batched: bad arguments"); return RDN_E_ARG; }
+  dim3 grid(64, n);
+  if (dtype == RDN_BF16) pack_weights_batched_kernel<bf16><<<grid, 256, 0, RDN_STREAM>>>(items, 64);
+  else pack_weights_batched_kernel<float><<<grid, 256, 0, RDN_STREAM>>>(items, 32);
+  return rdn_check_launch("rdn_pack_weights_batched");
+}
+
 extern "C" int rdn_pack_weights(int32_t mode, int32_t dtype, const float* w, int32_t d0, int32_t d1, int32_t kh,
                                 int32_t kw, int32_t pad0, int32_t pad1, void* out, int32_t rows_pad, int32_t kp,
-                                void* stream) {
+                                int32_t ck, void* stream) {
   if (!w || !out || mode < 0 || mode > 2 || kp % 64 || rows_pad % 128) { rdn_set_error("rdn_pack_weights: bad arguments"); return RDN_E_ARG; }
   const int taps = kh * kw;
-  if ((mode == RDN_PACK_CONV_FWD && (pad1 < d1 || rows_pad < d0 || taps * pad1 > kp)) ||
+  const int kc = chunk_kc(ck, dtype);
+  if (ck > 0) {
+    const int kside = mode == RDN_PACK_CONV_FWD ? pad1 : pad0;
+    if (taps != 9 || mode == RDN_PACK_GEMM_T || kside % ck || (kside / ck) * kc > kp) {
+      rdn_set_error("rdn_pack_weights: chunked pack needs a 3x3 conv mode and kp >= %d", (kside / ck) * kc);
+      return RDN_E_SHAPE;
+    }
+  } else if ((mode == RDN_PACK_CONV_FWD && (pad1 < d1 || rows_pad < d0 || taps * pad1 > kp)) ||
       (mode == RDN_PACK_CONV_DGRAD && (pad0 < d0 || rows_pad < d1 || taps * pad0 > kp)) ||
       (mode == RDN_PACK_GEMM_T && (pad0 < d0 || pad0 > kp || rows_pad < taps * d1))) {
     rdn_set_error("rdn_pack_weights: shape (mode=%d d0=%d d1=%d pad0=%d pad1=%d rows=%d kp=%d)", mode, d0, d1, pad0, pad1,
@@ -390,9 +461,9 @@ extern "C" int rdn_pack_weights(int32_t mode, int32_t dtype, const float* w, int
   }
   const int64_t total = (int64_t)rows_pad * kp;
   if (dtype == RDN_BF16)
-    pack_weights_kernel<bf16><<<grid_for(total, 256), 256, 0, RDN_STREAM>>>(mode, w, d0, d1, kh, kw, pad0, pad1, (bf16*)out, rows_pad, kp);
+    pack_weights_kernel<bf16><<<grid_for(total, 256), 256, 0, RDN_STREAM>>>(mode, w, d0, d1, kh, kw, pad0, pad1, (bf16*)out, rows_pad, kp, ck, kc);
   else
-    pack_weights_kernel<float><<<grid_for(total, 256), 256, 0, RDN_STREAM>>>(mode, w, d0, d1, kh, kw, pad0, pad1, (float*)out, rows_pad, kp);
+    pack_weights_kernel<float><<<grid_for(total, 256), 256, 0, RDN_STREAM>>>(mode, w, d0, d1, kh, kw, pad0, pad1, (float*)out, rows_pad, kp, ck, kc);
   return rdn_check_launch("rdn_pack_weights");
 }
 

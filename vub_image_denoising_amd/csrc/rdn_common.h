@@ -79,6 +79,11 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
   return (t + n) >> f.s;
 }
 
+int rdn_conv3_launch(const rdn_conv_desc* d, hipStream_t st);
+int rdn_conv3_chunk_impl(int cin, int dtype);
+int rdn_wgrad3_launch(const rdn_wgrad_desc* d, hipStream_t st);
+int rdn_wgrad3_splits(const rdn_wgrad_desc* d);
+
 // error plumbing (host)
 void rdn_set_error(const char* fmt, ...);
 int rdn_check_launch(const char* what);

@@ -273,15 +273,25 @@ class WeightPacks:
         named = dict(module.named_parameters())
         dev = fp.device
 
-        def mk(mode, w, d0, d1, kh, kw, pad0, pad1, rows, kp):
+        lib = H.lib()
+
+        def mk(mode, w, d0, d1, kh, kw, pad0, pad1, rows, kp, ck=0):
             out = torch.zeros(_ru(rows, 128), _ru(kp, 64), dtype=dtype, device=dev)
-            return (mode, w, d0, d1, kh, kw, pad0, pad1, out, out.shape[0], out.shape[1])
+            return (mode, w, d0, d1, kh, kw, pad0, pad1, out, out.shape[0], out.shape[1], ck)
+
+        def chunk(c):
+            ck, kp = lib.rdn_conv3_chunk(c, self.code), lib.rdn_conv3_packed_k(c, self.code)
+            if ck <= 0 or kp <= 0:
+                raise RuntimeError(f"conv3 K side of {c} channels unsupported")
+            return ck, kp
 
         for L in layers:
             w = named[L.name + ".weight"]
-            if L.kind == "c3":       # Conv2d 3x3 W[co][ci][3][3]
-                self.fwd[L.name] = mk(H.PACK_CONV_FWD, w, L.cout, L.cin, 3, 3, 0, L.cin_pad, L.cout, 9 * L.cin_pad)
-                self.dgrad[L.name] = mk(H.PACK_CONV_DGRAD, w, L.cout, L.cin, 3, 3, L.cout_pad, 0, L.cin, 9 * L.cout_pad)
+            if L.kind == "c3":       # Conv2d 3x3 W[co][ci][3][3], chunked K for the halo kernel
+                ck, kp = chunk(L.cin_pad)
+                self.fwd[L.name] = mk(H.PACK_CONV_FWD, w, L.cout, L.cin, 3, 3, 0, L.cin_pad, L.cout, kp, ck)
+                ck, kp = chunk(L.cout_pad)
+                self.dgrad[L.name] = mk(H.PACK_CONV_DGRAD, w, L.cout, L.cin, 3, 3, L.cout_pad, 0, L.cin, kp, ck)
             elif L.kind == "down":   # Conv2d 2x2 s2 W[co][ci][2][2]
                 self.fwd[L.name] = mk(H.PACK_CONV_FWD, w, L.cout, L.cin, 2, 2, 0, L.cin, L.cout, 4 * L.cin)
                 self.dgrad[L.name] = mk(H.PACK_GEMM_T, w, L.cout, L.cin, 2, 2, L.cout, 0, 4 * L.cin, L.cout)
@@ -289,6 +299,11 @@ class WeightPacks:
                 self.fwd[L.name] = mk(H.PACK_GEMM_T, w, L.cin, L.cout, 2, 2, L.cin, 0, 4 * L.cout, L.cin)
                 self.dgrad[L.name] = mk(H.PACK_CONV_FWD, w, L.cin, L.cout, 2, 2, 0, L.cout, L.cin, 4 * L.cout)
         self.items = list(self.fwd.values()) + list(self.dgrad.values())
+        arr = (H.PackItem * len(self.items))()
+        for i, (mode, w, d0, d1, kh, kw, pad0, pad1, out, rows, kp, ck) in enumerate(self.items):
+            arr[i] = H.PackItem(w.data_ptr(), out.data_ptr(), mode, d0, d1, kh, kw, pad0, pad1, rows, kp, ck)
+        raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+        self.items_dev = raw.to(dev)   # device copy of the descriptors: one launch packs all
 
     def attach(self, layers):
         for L in layers:
@@ -299,11 +314,8 @@ class WeightPacks:
         key = self.fp.version_key()
         if key == self.key:
             return
-        lib, st = H.lib(), H.stream_ptr()
-        for it in self.items:
-            mode, w, d0, d1, kh, kw, pad0, pad1, out, rows, kp = it
-            H.check(lib.rdn_pack_weights(mode, self.code, w.data_ptr(), d0, d1, kh, kw, pad0, pad1,
-                                         out.data_ptr(), rows, kp, st), "pack_weights")
+        H.check(H.lib().rdn_pack_weights_batched(self.items_dev.data_ptr(), len(self.items), self.code,
+                                                 H.stream_ptr()), "pack_weights_batched")
         self.key = key
 
 
@@ -357,6 +369,10 @@ class UNetEngine:
                 self.bufs["d" + name] = torch.zeros(self.P[lvl], ch, dtype=dtype, device=dev)
             dyp = max(self.P[self._out_level(L)] * L.cout_pad for L in layers)
             self.dyp = torch.zeros(dyp, dtype=dtype, device=dev)
+            lib = H.lib()
+            pws = max(lib.rdn_prelu_bwd_workspace_size(self.code, self.P[self._out_level(L)], L.cout, L.cout_pad)
+                      for L in layers)
+            self.pws = torch.zeros(max(pws // 4, 4), dtype=torch.float32, device=dev)
             self._build_bwd()
         self._build_info()
         self.token = 0
@@ -492,12 +508,37 @@ class UNetEngine:
         for L in self.layers:
             L.wgrad_desc.ws = self.ws.data_ptr()
 
+    def _kernel_key(self, desc):
+        """Name of the kernel template instantiation a conv descriptor launches
+        (matches the rocprofv3 kernel name, demangled)."""
+        dt = "bf16" if self.code == H.RDN_BF16 else "f32"
+        bn = 16 if desc.ncols <= 16 else 32 if desc.ncols <= 32 else 64 if desc.ncols <= 64 else 128
+        wmw = 4 if bn <= 32 else 2
+        if desc.gather == H.RDN_G_CONV3:
+            ck = H.lib().rdn_conv3_chunk(desc.cin, self.code)
+            bn = H.lib().rdn_conv3_pick_bn(desc.ncols)
+            wmw = 2 if bn in (64, 128) else 4
+            return f"conv3_halo_kernel<{dt},{bn},{wmw},{ck}>"
+        return f"conv_gemm_kernel<{dt},128,{bn},{wmw},{desc.gather}>"
+
+    def _wgrad_key(self, wg):
+        dt = "bf16" if self.code == H.RDN_BF16 else "f32"
+        if wg.gather == H.RDN_G_CONV3:
+            bm = 16 if wg.mdim <= 16 else 32 if wg.mdim <= 32 else 64
+            ck = H.lib().rdn_conv3_chunk(wg.ndim, self.code)
+            cap = (64 if bm <= 32 else 32) if self.code == H.RDN_BF16 else 32
+            while ck > cap:
+                ck //= 2
+            return f"wgrad3_halo_kernel<{dt},{bm},{ck}>"
+        bm = 16 if wg.mdim <= 16 else 32 if wg.mdim <= 32 else 64
+        bn = 64 if 4 * wg.ndim <= 64 else 128
+        wmw = 1 if bm == 16 else 2
+        return f"wgrad_kernel<{dt},{bm},{bn},{wmw},{wg.gather}>"
+
     def _build_info(self):
         """Per launch: kernel instantiation key + algorithmic FLOPs and bytes
         (each operand read once, each output written once)."""
-        dt = "bf16" if self.code == H.RDN_BF16 else "f32"
         es = 2 if self.code == H.RDN_BF16 else 4
-        gname = {H.RDN_G_CONV3: "conv3", H.RDN_G_S2: "s2", H.RDN_G_PIX: "pix"}
         for L in self.layers:
             olvl = self._out_level(L)
             Pout, Pin = self.P[olvl], self.P[L.level if L.kind == "up" else (L.level - 1 if L.kind == "down" else L.level)]
@@ -506,21 +547,14 @@ class UNetEngine:
                 macs = self.P[L.level] * 4 * L.cout * L.cin
             else:
                 macs = Pout * L.cout * taps * L.cin
-            fd = L.fwd_desc
-            bn = 16 if fd.ncols <= 16 else 32 if fd.ncols <= 32 else 64 if fd.ncols <= 64 else 128
             fwd_bytes = es * (Pin * L.cin + Pout * L.cout * (2 if self.train else 1) +
                               (Pout * L.cout if L.resid is not None else 0))
-            info = {"fwd": ("fwd", L.name, f"conv_gemm<{dt},128,{bn},{gname[fd.gather]}>", 2 * macs, fwd_bytes)}
+            info = {"fwd": ("fwd", L.name, self._kernel_key(L.fwd_desc), 2 * macs, fwd_bytes)}
             if self.train:
-                dd = L.dgrad_desc
-                bn = 16 if dd.ncols <= 16 else 32 if dd.ncols <= 32 else 64 if dd.ncols <= 64 else 128
                 dg_bytes = es * (Pout * L.cout + Pin * L.cin * (2 if L.accum else 1) +
                                  (Pin * L.resid_c if L.resid is not None else 0))
-                info["dgrad"] = ("dgrad", L.name, f"conv_gemm<{dt},128,{bn},{gname[dd.gather]}>", 2 * macs, dg_bytes)
-                wg = L.wgrad_desc
-                bm = 16 if wg.mdim <= 16 else 32 if wg.mdim <= 32 else 64
-                wbn = 64 if taps * wg.ndim <= 64 else 128
-                info["wgrad"] = ("wgrad", L.name, f"wgrad<{dt},{bm},{wbn},{gname[wg.gather]}>", 2 * macs,
+                info["dgrad"] = ("dgrad", L.name, self._kernel_key(L.dgrad_desc), 2 * macs, dg_bytes)
+                info["wgrad"] = ("wgrad", L.name, self._wgrad_key(L.wgrad_desc), 2 * macs,
                                  es * (Pout * L.cout + Pin * L.cin))
             L.extra["info"] = info
 
@@ -574,12 +608,13 @@ class UNetEngine:
             if L.ddst is None:
                 rc = lib.rdn_prelu_bwd(self.code, P, n, h, w, L.cout, L.cout_pad, None, 0, 0, dy.data_ptr(),
                                        pre.data_ptr(), pre.shape[1], self.named[L.act + ".weight"].data_ptr(),
-                                       dyp, ga.data_ptr(), gb.data_ptr(), st)
+                                       dyp, ga.data_ptr(), gb.data_ptr(), self.pws.data_ptr(), st)
             else:
                 dd = self.bufs[L.ddst.buf]
                 rc = lib.rdn_prelu_bwd(self.code, P, n, h, w, L.cout, L.cout_pad, dd.data_ptr(), dd.shape[1],
                                        L.ddst.c0, None, pre.data_ptr(), pre.shape[1],
-                                       self.named[L.act + ".weight"].data_ptr(), dyp, ga.data_ptr(), gb.data_ptr(), st)
+                                       self.named[L.act + ".weight"].data_ptr(), dyp, ga.data_ptr(), gb.data_ptr(),
+                                       self.pws.data_ptr(), st)
             if rc:
                 H.check(rc, f"prelu_bwd[{L.name}]")
             if L.name != "input_block.conv_1" or need_dx:
