@@ -80,6 +80,11 @@ typedef struct rdn_conv_desc {
   const void* res; int64_t res_ps; int32_t res_c0; int32_t res_climit;
   float* out_nchw; const float* res_nchw;
   int32_t bm, bn;        /* tile override, 0 = automatic                      */
+  /* optional PReLU-backward gate on the INPUT (RDN_G_CONV3 only): the gathered
+     x[p][c] becomes x[p][c] * (gate[p][c] > 0 ? 1 : gate_alpha[c]), i.e. the conv
+     consumes dYpre computed on the fly from dY and the saved PReLU input
+     (aten _prelu_kernel_backward fused into the input-gradient conv) */
+  const void* gate; int64_t gate_ps; const float* gate_alpha;
 } rdn_conv_desc;
 
 /* Implicit-GEMM convolution (MFMA) with the fused epilogue above. */
@@ -94,17 +99,28 @@ typedef struct rdn_wgrad_desc {
   const void* b; int64_t b_ps; int32_t b_c0; int32_t ndim;  /* per-tap columns, multiple of 8 */
   float* ws;               /* [splits][mdim][taps*ndim] partial sums           */
   int32_t splits;          /* 0 = automatic (see rdn_wgrad_splits)             */
+  /* optional PReLU-backward gate on operand A (RDN_G_CONV3 only), as in
+     rdn_conv_desc; with `part` non-NULL the kernel also writes per-split channel
+     partials part[split][0][m] = sum_{gate<=0} gate*A, part[split][1][m] = sum
+     gated A (dalpha / conv-bias gradients, summed by rdn_wgrad_reduce) */
+  const void* a_gate; int64_t a_gate_ps; const float* a_gate_alpha; float* part;
 } rdn_wgrad_desc;
 
 /* dW[m][tap][nd] partials = sum over pixels p of A[p][m] * B[gather(p,tap)][nd] */
 int rdn_conv_wgrad(const rdn_wgrad_desc* d, void* stream);
 /* split count the automatic mode would use, and the workspace it needs (bytes) */
 int rdn_wgrad_splits(const rdn_wgrad_desc* d);
+/* input-channel chunks (grid.y) of the 3x3 weight-gradient kernel: operand A is
+   read once per chunk, so the PReLU gate on A pays off only with 1 chunk */
+int rdn_wgrad_chunks(const rdn_wgrad_desc* d);
 int64_t rdn_wgrad_workspace_size(const rdn_wgrad_desc* d);
 /* grad[(m*ndim_real+nd)*taps+tap] (+)= sum_s ws[s][m][tap*ndim+nd] for nd < ndim_real:
-   the reference's OIHW (Conv2d) / IOHW (ConvTranspose2d) order */
+   the reference's OIHW (Conv2d) / IOHW (ConvTranspose2d) order.  With `part`
+   non-NULL also dalpha[m] += sum_s part[s][0][m], dbias[m] += sum_s part[s][1][m]
+   (fixed summation order: deterministic). */
 int rdn_wgrad_reduce(const float* ws, int32_t splits, int32_t mdim, int32_t ndim, int32_t ndim_real,
-                     int32_t taps, float* grad, int32_t accumulate, void* stream);
+                     int32_t taps, float* grad, int32_t accumulate,
+                     const float* part, float* dalpha, float* dbias, void* stream);
 
 /* PReLU backward (+ conv bias gradient) over a pixel grid of `pixels` pixels:
    dyp[p, c] = dy[p, c] * (pre[p, c] > 0 ? 1 : alpha[c])   (c < C; 0 for C <= c < cpad)

@@ -1,0 +1,99 @@
+"""Micro-benchmark of single conv launches (the network's real shapes at B=16,
+256x256) for one or more builds of librdunet_hip, interleaved in ONE process
+(MI355X_MICROARCH / cdna_hip_programming rule 24).
+
+  python scripts/kbench.py [lib1.so lib2.so ...]
+"""
+import ctypes as C
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+from vub_image_denoising_amd import _hip as H  # noqa: E402
+
+
+def load(path):
+    lib = C.CDLL(path)
+    for name, (res, args) in H.SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype, fn.argtypes = res, args
+    return lib
+
+
+# (name, N, H, W, buf_in, cin, cout_cols, kind) kind: fwd (bias+prelu+pre) | dgrad (store)
+SHAPES = [
+    ("L0 conv_0 32->16", 16, 256, 256, 80, 32, 16, "fwd"),
+    ("L0 conv_3 80->32", 16, 256, 256, 80, 80, 32, "fwd"),
+    ("L0 dgrad3 32->80", 16, 256, 256, 32, 32, 80, "dgrad"),
+    ("L1 conv_3 160->64", 16, 128, 128, 160, 160, 64, "fwd"),
+    ("L1 dgrad3 64->160", 16, 128, 128, 64, 64, 160, "dgrad"),
+    ("L2 conv_3 320->128", 16, 64, 64, 320, 320, 128, "fwd"),
+    ("L2 dgrad3 128->320", 16, 64, 64, 128, 128, 320, "dgrad"),
+    ("L3 conv_3 640->256", 16, 32, 32, 640, 640, 256, "fwd"),
+    ("L3 dgrad3 256->640", 16, 32, 32, 256, 256, 640, "dgrad"),
+]
+
+
+def setup(lib, shp, dt):
+    name, N, Hh, Ww, cs, cin, cols, kind = shp
+    code = H.dtype_code(dt)
+    P = N * Hh * Ww
+    x = torch.randn(P, cs, device="cuda").to(dt)
+    w = torch.randn(cols, cin, 3, 3, device="cuda") * 0.05
+    ck = lib.rdn_conv3_chunk(cin, code)
+    kp = lib.rdn_conv3_packed_k(cin, code)
+    rows = (cols + 127) // 128 * 128
+    wp = torch.zeros(rows, kp, dtype=dt, device="cuda")
+    H.check(lib.rdn_pack_weights(H.PACK_CONV_FWD, code, w.data_ptr(), cols, cin, 3, 3, 0, cin, wp.data_ptr(), rows, kp,
+                                 ck, torch.cuda.current_stream().cuda_stream))
+    b = torch.zeros(cols, device="cuda")
+    a = torch.full((cols,), 0.25, device="cuda")
+    out = torch.zeros(P, cols, dtype=dt, device="cuda")
+    pre = torch.zeros(P, cols, dtype=dt, device="cuda")
+    flags = (H.EPI_BIAS | H.EPI_PRELU | H.EPI_STORE_PRE) if kind == "fwd" else 0
+    d = H.ConvDesc(dtype=code, gather=H.RDN_G_CONV3, flags=flags, n=N, h=Hh, w=Ww, hin=Hh, win=Ww, cin=cin,
+                   x=x.data_ptr(), x_ps=cs, x_c0=0, wp=wp.data_ptr(), kp=kp, ncols=cols, cout=cols,
+                   bias=b.data_ptr(), alpha=a.data_ptr(), out=out.data_ptr(), out_ps=cols, out_c0=0,
+                   pre=pre.data_ptr(), pre_ps=cols, bn=int(os.environ.get("KB_BN", "0")))
+    flops = 2.0 * P * cols * 9 * cin
+    es = 2 if dt == torch.bfloat16 else 4
+    byts = es * P * (cin + cols * (2 if kind == "fwd" else 1))
+    return d, (x, w, wp, b, a, out, pre), flops, byts
+
+
+def main():
+    libs = sys.argv[1:] or [H.LIB_PATH]
+    L = [load(p) for p in libs]
+    dt = torch.bfloat16 if os.environ.get("KB_DT", "bf16") == "bf16" else torch.float32
+    st = torch.cuda.current_stream().cuda_stream
+    reps = int(os.environ.get("KB_REPS", "20"))
+    print(f"{'shape':24s} " + " ".join(f"{os.path.basename(p)[:22]:>24s}" for p in libs))
+    for shp in SHAPES:
+        res = []
+        setups = [setup(lib, shp, dt) for lib in L]
+        times = [[] for _ in L]
+        for rnd in range(3):
+            for i, lib in enumerate(L):
+                d = setups[i][0]
+                for _ in range(2):
+                    lib.rdn_conv_fwd(C.byref(d), st)
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                for _ in range(reps):
+                    rc = lib.rdn_conv_fwd(C.byref(d), st)
+                e.record()
+                torch.cuda.synchronize()
+                assert rc == 0, lib.rdn_last_error()
+                times[i].append(s.elapsed_time(e) / reps)
+        for i in range(len(L)):
+            t = min(times[i])
+            fl, by = setups[i][2], setups[i][3]
+            res.append(f"{t * 1e3:7.1f}us {fl / t / 1e9:6.0f}TF {by / t / 1e6:5.0f}GB")
+        print(f"{shp[0]:24s} " + " ".join(f"{r:>24s}" for r in res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -169,7 +169,8 @@ def _wgrad(dt, gather, N, h, w, hin, win, A, a_ps, a_c0, mdim, B, b_ps, b_c0, nd
     d.ws = ws.data_ptr()
     H.check(lib.rdn_conv_wgrad(C.byref(d), H.stream_ptr()))
     g = torch.zeros(mdim * ndim_real * taps, device="cuda")
-    H.check(lib.rdn_wgrad_reduce(ws.data_ptr(), ns, mdim, ndim, ndim_real, taps, g.data_ptr(), 0, H.stream_ptr()))
+    H.check(lib.rdn_wgrad_reduce(ws.data_ptr(), ns, mdim, ndim, ndim_real, taps, g.data_ptr(), 0, None, None, None,
+                                 H.stream_ptr()))
     torch.cuda.synchronize()
     return g
 
@@ -328,3 +329,65 @@ def test_charbonnier_clip_adam_combine():
     xr = x.cpu() - ((1 - 0.75) * f1.cpu() + 0.75 * y.cpu()) + ((1 - 0.5) * f2.cpu() + 0.5 * y.cpu())
     Fn.sampling_combine(x, f1, f2, y, 0.75, 0.5)
     assert _rel(x, xr) < 1e-6
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_fused_prelu_gate_matches_separate_pass(dt):
+    """dgrad/wgrad with the PReLU-backward gate (dY, saved PReLU input) equal the
+    unfused rdn_prelu_bwd -> dYpre -> dgrad/wgrad pipeline; the dalpha/dbias
+    partials summed in rdn_wgrad_reduce match rdn_prelu_bwd's."""
+    lib = H.lib()
+    N, Hh, Ww, cin, Cs, cout, Cd = 2, 16, 32, 48, 80, 16, 80
+    P = N * Hh * Ww
+    code = H.dtype_code(dt)
+    st = H.stream_ptr()
+    x = torch.randn(P, Cs, device="cuda").to(dt)            # conv input (dense buffer)
+    dyb = torch.randn(P, Cd, device="cuda").to(dt)          # gradient buffer, slice [48, 64)
+    pre = torch.randn(P, cout, device="cuda").to(dt)
+    pre[::5] = 0
+    a = torch.rand(cout, device="cuda")
+    w = torch.randn(cout, cin, 3, 3, device="cuda") * 0.05
+    wpd = _pack(H.PACK_CONV_DGRAD, w, cout, cin, 3, 3, cout, 0, cin, 9 * cout, dt)
+    # unfused
+    dyp = torch.zeros(P, cout, dtype=dt, device="cuda")
+    da1, db1 = torch.zeros(cout, device="cuda"), torch.zeros(cout, device="cuda")
+    pws = torch.zeros(lib.rdn_prelu_bwd_workspace_size(code, P, cout, cout) // 4 + 4096, device="cuda")
+    H.check(lib.rdn_prelu_bwd(code, P, N, Hh, Ww, cout, cout, dyb.data_ptr(), Cd, 48, None, pre.data_ptr(), cout,
+                              a.data_ptr(), dyp.data_ptr(), da1.data_ptr(), db1.data_ptr(), pws.data_ptr(), st))
+
+    def dgrad(xp, xps, xc0, gate):
+        out = torch.zeros(P, Cs, dtype=dt, device="cuda")
+        d = H.ConvDesc(dtype=code, gather=H.RDN_G_CONV3, flags=0, n=N, h=Hh, w=Ww, hin=Hh, win=Ww, cin=cout, x=xp,
+                       x_ps=xps, x_c0=xc0, wp=wpd.data_ptr(), kp=wpd.shape[1], ncols=cin, cout=cin,
+                       out=out.data_ptr(), out_ps=Cs, out_c0=0)
+        if gate:
+            d.gate, d.gate_ps, d.gate_alpha = pre.data_ptr(), cout, a.data_ptr()
+        H.check(lib.rdn_conv_fwd(C.byref(d), st))
+        return out
+
+    def wgrad(ap, aps, ac0, gate, da, db):
+        wd = H.WgradDesc(dtype=code, gather=H.RDN_G_CONV3, n=N, h=Hh, w=Ww, hin=Hh, win=Ww, a=ap, a_ps=aps, a_c0=ac0,
+                         mdim=cout, b=x.data_ptr(), b_ps=Cs, b_c0=0, ndim=cin)
+        ns = lib.rdn_wgrad_splits(C.byref(wd))
+        wd.splits = ns
+        ws = torch.zeros(lib.rdn_wgrad_workspace_size(C.byref(wd)) // 4, device="cuda")
+        part = torch.zeros(ns * 2 * cout, device="cuda")
+        wd.ws = ws.data_ptr()
+        if gate:
+            wd.a_gate, wd.a_gate_ps, wd.a_gate_alpha, wd.part = pre.data_ptr(), cout, a.data_ptr(), part.data_ptr()
+        g = torch.zeros(cout * cin * 9, device="cuda")
+        H.check(lib.rdn_conv_wgrad(C.byref(wd), st))
+        H.check(lib.rdn_wgrad_reduce(ws.data_ptr(), ns, cout, cin, cin, 9, g.data_ptr(), 0,
+                                     part.data_ptr() if gate else None, da.data_ptr() if gate else None,
+                                     db.data_ptr() if gate else None, st))
+        return g
+
+    o1 = dgrad(dyp.data_ptr(), cout, 0, False)
+    g1 = wgrad(dyp.data_ptr(), cout, 0, False, None, None)
+    da2, db2 = torch.zeros(cout, device="cuda"), torch.zeros(cout, device="cuda")
+    o2 = dgrad(dyb.data_ptr(), Cd, 48, True)
+    g2 = wgrad(dyb.data_ptr(), Cd, 48, True, da2, db2)
+    torch.cuda.synchronize()
+    assert torch.equal(o1, o2)
+    assert torch.equal(g1, g2)
+    assert _rel(da2, da1) < 1e-5 and _rel(db2, db1) < 1e-5

@@ -14,7 +14,7 @@ import threading
 import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "librdunet_hip.so")
+LIB_PATH = os.environ.get("RDN_LIB") or os.path.join(HERE, "librdunet_hip.so")
 
 RDN_F32, RDN_BF16 = 0, 1
 RDN_G_CONV3, RDN_G_S2, RDN_G_PIX = 0, 1, 2
@@ -36,6 +36,7 @@ class ConvDesc(C.Structure):
         ("res", _vp), ("res_ps", _i64), ("res_c0", _i32), ("res_climit", _i32),
         ("out_nchw", _vp), ("res_nchw", _vp),
         ("bm", _i32), ("bn", _i32),
+        ("gate", _vp), ("gate_ps", _i64), ("gate_alpha", _vp),
     ]
 
 
@@ -45,6 +46,7 @@ class WgradDesc(C.Structure):
         ("a", _vp), ("a_ps", _i64), ("a_c0", _i32), ("mdim", _i32),
         ("b", _vp), ("b_ps", _i64), ("b_c0", _i32), ("ndim", _i32),
         ("ws", _vp), ("splits", _i32),
+        ("a_gate", _vp), ("a_gate_ps", _i64), ("a_gate_alpha", _vp), ("part", _vp),
     ]
 
 
@@ -58,8 +60,9 @@ SIGNATURES = {
     "rdn_conv_fwd": (_i32, [C.POINTER(ConvDesc), _vp]),
     "rdn_conv_wgrad": (_i32, [C.POINTER(WgradDesc), _vp]),
     "rdn_wgrad_splits": (_i32, [C.POINTER(WgradDesc)]),
+    "rdn_wgrad_chunks": (_i32, [C.POINTER(WgradDesc)]),
     "rdn_wgrad_workspace_size": (_i64, [C.POINTER(WgradDesc)]),
-    "rdn_wgrad_reduce": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _vp, _i32, _vp]),
+    "rdn_wgrad_reduce": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _vp, _i32, _vp, _vp, _vp, _vp]),
     "rdn_prelu_bwd": (_i32, [_i32, _i64, _i32, _i32, _i32, _i32, _i32, _vp, _i64, _i32, _vp, _vp, _i64, _vp,
                              _vp, _vp, _vp, _vp, _vp]),
     "rdn_prelu_bwd_workspace_size": (_i64, [_i32, _i64, _i32, _i32]),

@@ -27,8 +27,10 @@ constexpr int ROWB = 160;                  // B-stage row: 128 B + 32 B pad (con
 
 template <int CKB> struct HaloRow { static constexpr int V = CKB >= 64 ? CKB + 32 : CKB; };
 
-template <typename T, int BN, int WMW, int CK>
-__global__ __launch_bounds__(NT, 2) void conv3_halo_kernel(rdn_conv_desc d, int tiles_x, int tiles_y) {
+// occupancy request: narrow tiles keep 2 waves/SIMD, wide tiles let the
+// register allocator use up to 512 VGPRs (measured faster: scripts/kbench.py)
+template <typename T, int BN, int WMW, int CK, bool GATE>
+__global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_conv_desc d, int tiles_x, int tiles_y) {
   constexpr int ES = sizeof(T);
   constexpr int VEC = TypeInfo<T>::VEC;
   constexpr int SK = 128 / ES;                       // k per stage
@@ -70,21 +72,36 @@ __global__ __launch_bounds__(NT, 2) void conv3_halo_kernel(rdn_conv_desc d, int 
   const int nch = d.cin / CK;
   const int nst = nch * SPC;
 
-  // ---- halo loader: unit u -> (halo pixel, 16-B channel group)
+  // ---- halo loader: unit u -> (halo pixel, 16-B channel group).  With GATE
+  // the unit is dY and becomes dYpre = dY * (pre > 0 ? 1 : alpha) when it is
+  // written to LDS (PReLU backward fused into the input-gradient conv).
+  static_assert(NT % HU == 0, "fixed channel group per thread");
   u32x4 hreg[H_IT];
+  u32x4 greg[GATE ? H_IT : 1];
+  float galpha[GATE ? VEC : 1];
+  const T* __restrict__ G = (const T*)d.gate;
   auto load_halo = [&](int c) {
+    if constexpr (GATE) {
+      const int ch = c * CK + (tid % HU) * VEC;
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) galpha[q] = d.gate_alpha[ch + q];
+    }
 #pragma unroll
     for (int it = 0; it < H_IT; ++it) {
       const int u = tid + it * NT;
-      u32x4 v = {0u, 0u, 0u, 0u};
+      u32x4 v = {0u, 0u, 0u, 0u}, gv = {0u, 0u, 0u, 0u};
       if (u < H_UNITS) {
         const int hp = u / HU, cu = u - hp * HU;
         const int hy = hp / (TW + 2), hx = hp - hy * (TW + 2);
         const int yy = y0 + hy - 1, xx = x0 + hx - 1;
-        if (yy >= 0 && yy < H && xx >= 0 && xx < W)
-          v = *(const u32x4*)(X + (((int64_t)nimg * H + yy) * W + xx) * d.x_ps + d.x_c0 + c * CK + cu * VEC);
+        if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
+          const int64_t pix = ((int64_t)nimg * H + yy) * W + xx;
+          v = *(const u32x4*)(X + pix * d.x_ps + d.x_c0 + c * CK + cu * VEC);
+          if constexpr (GATE) gv = *(const u32x4*)(G + pix * d.gate_ps + c * CK + cu * VEC);
+        }
       }
       hreg[it] = v;
+      if constexpr (GATE) greg[it] = gv;
     }
   };
   auto store_halo = [&]() {
@@ -93,7 +110,16 @@ __global__ __launch_bounds__(NT, 2) void conv3_halo_kernel(rdn_conv_desc d, int 
       const int u = tid + it * NT;
       if (u < H_UNITS) {
         const int hp = u / HU, cu = u - hp * HU;
-        *(u32x4*)(halo + hp * HROW + cu * 16) = hreg[it];
+        u32x4 v = hreg[it];
+        if constexpr (GATE) {
+          float dy[VEC], pr[VEC];
+          Unit16<T>::unpack(v, dy);
+          Unit16<T>::unpack(greg[it], pr);
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) dy[q] = pr[q] > 0.f ? dy[q] : galpha[q] * dy[q];
+          v = Unit16<T>::pack(dy);
+        }
+        *(u32x4*)(halo + hp * HROW + cu * 16) = v;
       }
     }
   };
@@ -126,17 +152,8 @@ __global__ __launch_bounds__(NT, 2) void conv3_halo_kernel(rdn_conv_desc d, int 
   // tile-local pixel of m-tile i, lane row r: (py, px) = (wm*WTM/16 + i, r)
   const int py0 = wm * (WTM / 16);
 
-  load_halo(0);
-  store_halo();
-  load_b(0);
-  store_b(0);
-  __syncthreads();
-
-  for (int s = 0; s < nst; ++s) {
+  auto compute = [&](int s) {
     const int c = s / SPC, j = s - c * SPC;
-    const bool last_of_chunk = (j == SPC - 1);
-    if (j == 0 && c + 1 < nch) load_halo(c + 1);
-    if (s + 1 < nst) load_b(s + 1);
     const int buf = s & 1;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -169,13 +186,74 @@ __global__ __launch_bounds__(NT, 2) void conv3_halo_kernel(rdn_conv_desc d, int 
           }
         }
     }
-    if (s + 1 < nst) store_b(buf ^ 1);
+  };
+
+  load_halo(0);
+  store_halo();
+#if defined(RDN_HALO_PF2)
+  // weights prefetched TWO stages ahead in two register sets (even / odd stage)
+  u32x4 breg2[B_IT];
+  auto load_b2 = [&](int s, u32x4* R) {
+    const int c = s / SPC, j = s - c * SPC;
+#pragma unroll
+    for (int it = 0; it < B_IT; ++it) {
+      const int u = tid + it * NT;
+      if (u < B_UNITS)
+        R[it] = *(const u32x4*)(WP + (int64_t)(n0 + (u >> 3)) * d.kp + (int64_t)c * KC + j * SK + ku * VEC);
+    }
+  };
+  auto store_b2 = [&](int buf, const u32x4* R) {
+#pragma unroll
+    for (int it = 0; it < B_IT; ++it) {
+      const int u = tid + it * NT;
+      if (u < B_UNITS) *(u32x4*)(ldsB(buf) + (u >> 3) * ROWB + ku * 16) = R[it];
+    }
+  };
+  load_b2(0, breg);
+  store_b2(0, breg);
+  if (nst > 1) load_b2(1, breg2);
+  __syncthreads();
+  auto step = [&](int s, u32x4* Rfree, const u32x4* Rnext) {
+    const int c = s / SPC, j = s - c * SPC;
+    if (j == 0 && c + 1 < nch) load_halo(c + 1);
+    if (s + 2 < nst) load_b2(s + 2, Rfree);
+    compute(s);
+    if (s + 1 < nst) store_b2((s + 1) & 1, Rnext);
+    __syncthreads();
+    if (j == SPC - 1 && c + 1 < nch) {
+      store_halo();
+      __syncthreads();
+    }
+  };
+  int s = 0;
+  for (; s + 1 < nst; s += 2) {
+    step(s, breg, breg2);
+    step(s + 1, breg2, breg);
+  }
+  if (s < nst) step(s, breg, breg2);
+#else
+  load_b(0);
+  store_b(0);
+  __syncthreads();
+
+  for (int s = 0; s < nst; ++s) {
+    const int c = s / SPC, j = s - c * SPC;
+    const bool last_of_chunk = (j == SPC - 1);
+    if (j == 0 && c + 1 < nch) load_halo(c + 1);
+#if !defined(RDN_HALO_NOLOADB)
+    if (s + 1 < nst) load_b(s + 1);
+#endif
+    compute(s);
+#if !defined(RDN_HALO_NOLOADB)
+    if (s + 1 < nst) store_b((s & 1) ^ 1);
+#endif
     __syncthreads();
     if (last_of_chunk && c + 1 < nch) {
       store_halo();
       __syncthreads();
     }
   }
+#endif
 #undef ldsB
 
   // ---- epilogue: fp32 tile through LDS, then 16-byte NHWC stores
@@ -273,12 +351,16 @@ template <typename T, int BN, int WMW, int CK>
 int launch_h(const rdn_conv_desc* d, hipStream_t st) {
   const int tiles_x = (d->w + TW - 1) / TW, tiles_y = (d->h + TH - 1) / TH;
   dim3 grid((unsigned)(d->n * tiles_x * tiles_y), (unsigned)((d->ncols + BN - 1) / BN));
-  conv3_halo_kernel<T, BN, WMW, CK><<<grid, NT, 0, st>>>(*d, tiles_x, tiles_y);
+  if (d->gate) conv3_halo_kernel<T, BN, WMW, CK, true><<<grid, NT, 0, st>>>(*d, tiles_x, tiles_y);
+  else conv3_halo_kernel<T, BN, WMW, CK, false><<<grid, NT, 0, st>>>(*d, tiles_x, tiles_y);
   return rdn_check_launch("rdn_conv_fwd(conv3)");
 }
 
-// BN choice: the candidate minimising padded columns ceil(ncols/BN)*BN, ties to the larger BN
+// BN choice: 64 for wide outputs (more blocks on the small deep levels; measured
+// best on the L1-L3 shapes), else the candidate minimising padded columns
+// ceil(ncols/BN)*BN, ties to the larger BN
 static int pick_bn(int ncols) {
+  if (ncols > 128) return 64;
   static const int cands[] = {128, 96, 80, 64, 48, 32, 16};
   int best = 128, waste = 1 << 30;
   for (int b : cands) {
@@ -328,6 +410,9 @@ extern "C" int rdn_conv3_pick_bn(int32_t ncols) { return pick_bn(ncols); }
 
 int rdn_conv3_launch(const rdn_conv_desc* d, hipStream_t st) {
   const int ck = rdn_conv3_chunk_impl(d->cin, d->dtype);
+  if (d->gate && (!d->gate_alpha || d->gate_ps % (d->dtype == RDN_BF16 ? 8 : 4) || ((uintptr_t)d->gate & 15))) {
+    rdn_set_error("rdn_conv_fwd(conv3): gate needs alpha and 16-byte aligned rows"); return RDN_E_ARG;
+  }
   if (ck < 0) { rdn_set_error("rdn_conv_fwd(conv3): cin=%d not a multiple of 8", d->cin); return RDN_E_SHAPE; }
   if (d->kp < rdn_conv3_packed_k(d->cin, d->dtype)) {
     rdn_set_error("rdn_conv_fwd(conv3): kp=%d < packed K %d (pack with ck=%d)", d->kp,

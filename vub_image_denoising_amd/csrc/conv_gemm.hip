@@ -283,5 +283,6 @@ extern "C" int rdn_conv_fwd(const rdn_conv_desc* d, void* stream) {
   }
   hipStream_t st = (hipStream_t)stream;
   if (d->gather == RDN_G_CONV3) return rdn_conv3_launch(d, st);  // LDS-halo kernel (conv3_halo.hip)
+  if (d->gate) { rdn_set_error("rdn_conv_fwd: the PReLU gate is supported for RDN_G_CONV3 only"); return RDN_E_ARG; }
   return d->dtype == RDN_BF16 ? launch_typed<bf16>(d, st) : launch_typed<float>(d, st);
 }

@@ -188,7 +188,26 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(rdn_wgrad_desc d, FastDiv fd_
 // [m][nd][tap] (OIHW / IOHW).
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int mdim, int ndim,
                                                            int ndim_real, int taps, float* __restrict__ grad,
-                                                           int accumulate, int sl_count) {
+                                                           int accumulate, int sl_count, const float* __restrict__ part,
+                                                           float* __restrict__ dalpha, float* __restrict__ dbias) {
+  if (blockIdx.y == 1) {  // fused-PReLU partials: one block per (channel, dalpha|dbias), fixed order
+    if (blockIdx.x >= 2 * mdim) return;
+    const int which = blockIdx.x / mdim, m = blockIdx.x - which * mdim;
+    float s = 0.f;
+    for (int z = threadIdx.x; z < splits; z += 256) s += part[((int64_t)z * 2 + which) * mdim + m];
+    __shared__ float red1[256];
+    red1[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if (threadIdx.x < o) red1[threadIdx.x] += red1[threadIdx.x + o];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+      float* dst = which ? dbias : dalpha;
+      if (dst) dst[m] += red1[0];
+    }
+    return;
+  }
   const int cpb = 256 / sl_count;
   const int cc = threadIdx.x % cpb, sl = threadIdx.x / cpb;
   const int ncol = taps * ndim;
@@ -272,6 +291,11 @@ extern "C" int rdn_wgrad_splits(const rdn_wgrad_desc* d) {
   return d->gather == RDN_G_CONV3 ? rdn_wgrad3_splits(d) : auto_splits(d);
 }
 
+extern "C" int rdn_wgrad_chunks(const rdn_wgrad_desc* d) {
+  if (!d) return RDN_E_ARG;
+  return d->gather == RDN_G_CONV3 ? rdn_wgrad3_chunks(d) : 1;
+}
+
 extern "C" int64_t rdn_wgrad_workspace_size(const rdn_wgrad_desc* d) {
   if (!d) return RDN_E_ARG;
   const int taps = d->gather == RDN_G_CONV3 ? 9 : 4;
@@ -300,7 +324,8 @@ extern "C" int rdn_conv_wgrad(const rdn_wgrad_desc* d, void* stream) {
 }
 
 extern "C" int rdn_wgrad_reduce(const float* ws, int32_t splits, int32_t mdim, int32_t ndim, int32_t ndim_real,
-                                int32_t taps, float* grad, int32_t accumulate, void* stream) {
+                                int32_t taps, float* grad, int32_t accumulate, const float* part, float* dalpha,
+                                float* dbias, void* stream) {
   if (!ws || !grad || splits <= 0 || mdim <= 0 || ndim <= 0 || ndim_real <= 0 || ndim_real > ndim || taps <= 0) {
     rdn_set_error("rdn_wgrad_reduce: bad arguments"); return RDN_E_ARG;
   }
@@ -308,9 +333,11 @@ extern "C" int rdn_wgrad_reduce(const float* ws, int32_t splits, int32_t mdim, i
   int sl = 1;
   while (sl < 16 && sl < splits) sl <<= 1;
   const int cpb = 256 / sl;
-  const int64_t blocks = (total + cpb - 1) / cpb;
+  int64_t blocks = (total + cpb - 1) / cpb;
+  if (part && blocks < 2 * mdim) blocks = 2 * mdim;
   if (blocks > 0x7fffffff) { rdn_set_error("rdn_wgrad_reduce: too large"); return RDN_E_SHAPE; }
-  wgrad_reduce_kernel<<<(unsigned)blocks, 256, 0, (hipStream_t)stream>>>(ws, splits, mdim, ndim, ndim_real, taps, grad,
-                                                                         accumulate, sl);
+  dim3 grid((unsigned)blocks, part ? 2 : 1);
+  wgrad_reduce_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(ws, splits, mdim, ndim, ndim_real, taps, grad, accumulate,
+                                                            sl, part, dalpha, dbias);
   return rdn_check_launch("rdn_wgrad_reduce");
 }

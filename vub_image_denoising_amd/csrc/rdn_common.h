@@ -83,6 +83,7 @@ int rdn_conv3_launch(const rdn_conv_desc* d, hipStream_t st);
 int rdn_conv3_chunk_impl(int cin, int dtype);
 int rdn_wgrad3_launch(const rdn_wgrad_desc* d, hipStream_t st);
 int rdn_wgrad3_splits(const rdn_wgrad_desc* d);
+int rdn_wgrad3_chunks(const rdn_wgrad_desc* d);
 
 // error plumbing (host)
 void rdn_set_error(const char* fmt, ...);

@@ -29,9 +29,14 @@ constexpr int HP = (TH + 2) * (TW + 2);
 
 // conflict-free row strides for ds_read_b64_tr_b16 with the interleaved
 // k order (see header): data bytes -> stride
-constexpr int tr_stride(int bytes) { return bytes <= 32 ? bytes : bytes == 64 ? 96 : bytes == 128 ? 160 : bytes + 32; }
+constexpr int tr_stride(int bytes) {
+  return bytes <= 32 ? bytes : bytes == 64 ? 96 : bytes == 96 ? 96 : bytes == 128 ? 160 : bytes == 160 ? 160
+       : bytes == 192 ? 224 : bytes + 32;
+}
+// fp32 (ds_read_b32, rows g and g+1 in one half-wave): stride = 64 (mod 128) bytes
+constexpr int f32_stride(int bytes) { return bytes % 128 <= 64 ? bytes - bytes % 128 + 64 : bytes - bytes % 128 + 192; }
 
-template <typename T, int BM, int CK>
+template <typename T, int BM, int CK, bool GATE>
 __global__ __launch_bounds__(NT, 2) void wgrad3_halo_kernel(rdn_wgrad_desc d, int tiles_x, int tiles_y, int ntiles,
                                                             int tiles_per_block) {
   constexpr int ES = sizeof(T);
@@ -40,12 +45,14 @@ __global__ __launch_bounds__(NT, 2) void wgrad3_halo_kernel(rdn_wgrad_desc d, in
   constexpr int NT_ALL = (NCOL + 15) / 16;
   constexpr int NTW = (NT_ALL + 3) / 4;     // n-tiles per wave
   constexpr int MT = BM / 16;
-  constexpr int DROW = ES == 2 ? tr_stride(BM * ES) : BM * ES + 16;
-  constexpr int HROW = ES == 2 ? tr_stride(CK * ES) : CK * ES + 16;
+  constexpr int DROW = ES == 2 ? tr_stride(BM * ES) : f32_stride(BM * ES);
+  constexpr int HROW = ES == 2 ? tr_stride(CK * ES) : f32_stride(CK * ES);
   constexpr int D_UNITS = TP * (BM / VEC), H_UNITS = HP * (CK / VEC);
   constexpr int D_IT = (D_UNITS + NT - 1) / NT, H_IT = (H_UNITS + NT - 1) / NT;
   constexpr int D_BYTES = TP * DROW;
-  __shared__ __attribute__((aligned(16))) unsigned char lds[D_BYTES + HP * HROW];
+  constexpr int MAIN_BYTES = D_BYTES + HP * HROW;
+  constexpr int RED_BYTES = GATE ? 2 * NT * VEC * 4 : 0;   // dalpha/dbias partial reduction
+  __shared__ __attribute__((aligned(16))) unsigned char lds[MAIN_BYTES > RED_BYTES ? MAIN_BYTES : RED_BYTES];
   unsigned char* const dyl = lds;
   unsigned char* const hal = lds + D_BYTES;
 
@@ -60,6 +67,22 @@ __global__ __launch_bounds__(NT, 2) void wgrad3_halo_kernel(rdn_wgrad_desc d, in
   const int H = d.h, W = d.w;
 
   u32x4 dreg[D_IT], hreg[H_IT];
+  // PReLU-backward gate on A (dY -> dYpre) + dalpha / dbias partials
+  static_assert(NT % (BM / VEC) == 0, "fixed channel group per thread");
+  u32x4 greg[GATE ? D_IT : 1];
+  const T* __restrict__ G = (const T*)d.a_gate;
+  const int acg = tid % (BM / VEC);           // this thread's A channel group
+  float galpha[GATE ? VEC : 1], sa[GATE ? VEC : 1], sb[GATE ? VEC : 1];
+  const bool do_part = GATE && d.part != nullptr && blockIdx.y == 0;
+  if constexpr (GATE) {
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) {
+      const int m = m0 + acg * VEC + q;
+      galpha[q] = m < d.mdim ? d.a_gate_alpha[m] : 0.f;
+      sa[q] = 0.f;
+      sb[q] = 0.f;
+    }
+  }
   auto load_tile = [&](int t) {
     const int tx = t % tiles_x, r1 = t / tiles_x;
     const int ty = r1 % tiles_y, nimg = r1 / tiles_y;
@@ -67,15 +90,19 @@ __global__ __launch_bounds__(NT, 2) void wgrad3_halo_kernel(rdn_wgrad_desc d, in
 #pragma unroll
     for (int it = 0; it < D_IT; ++it) {
       const int u = tid + it * NT;
-      u32x4 v = {0u, 0u, 0u, 0u};
+      u32x4 v = {0u, 0u, 0u, 0u}, gv = {0u, 0u, 0u, 0u};
       if (u < D_UNITS) {
         const int p = u / (BM / VEC), cu = u - p * (BM / VEC);
         const int yy = y0 + p / TW, xx = x0 + p % TW;
         const int m = m0 + cu * VEC;
-        if (yy < H && xx < W && m < d.mdim)
-          v = *(const u32x4*)(A + (((int64_t)nimg * H + yy) * W + xx) * d.a_ps + d.a_c0 + m);
+        if (yy < H && xx < W && m < d.mdim) {
+          const int64_t pix = ((int64_t)nimg * H + yy) * W + xx;
+          v = *(const u32x4*)(A + pix * d.a_ps + d.a_c0 + m);
+          if constexpr (GATE) gv = *(const u32x4*)(G + pix * d.a_gate_ps + m);
+        }
       }
       dreg[it] = v;
+      if constexpr (GATE) greg[it] = gv;
     }
 #pragma unroll
     for (int it = 0; it < H_IT; ++it) {
@@ -97,7 +124,24 @@ __global__ __launch_bounds__(NT, 2) void wgrad3_halo_kernel(rdn_wgrad_desc d, in
       const int u = tid + it * NT;
       if (u < D_UNITS) {
         const int p = u / (BM / VEC), cu = u - p * (BM / VEC);
-        *(u32x4*)(dyl + p * DROW + cu * 16) = dreg[it];
+        u32x4 v = dreg[it];
+        if constexpr (GATE) {
+          float dy[VEC], pr[VEC];
+          Unit16<T>::unpack(v, dy);
+          Unit16<T>::unpack(greg[it], pr);
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) {
+            const bool pos = pr[q] > 0.f;
+            if (!pos) sa[q] += pr[q] * dy[q];
+            dy[q] = pos ? dy[q] : galpha[q] * dy[q];
+          }
+          v = Unit16<T>::pack(dy);
+          if (do_part) {  // dbias sums dYpre before its rounding to T, as rdn_prelu_bwd does
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) sb[q] += dy[q];
+          }
+        }
+        *(u32x4*)(dyl + p * DROW + cu * 16) = v;
       }
     }
 #pragma unroll
@@ -187,6 +231,32 @@ __global__ __launch_bounds__(NT, 2) void wgrad3_halo_kernel(rdn_wgrad_desc d, in
     }
   }
 
+  if constexpr (GATE) {
+    if (d.part != nullptr && blockIdx.y == 0) {
+      // per-block channel partials -> part[split][0|1][m] (LDS reduce, fixed order)
+      float* red = (float*)lds;  // reuse: the tile loop ended with a barrier
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) {
+        red[tid * VEC + q] = sa[q];
+        red[NT * VEC + tid * VEC + q] = sb[q];
+      }
+      __syncthreads();
+      constexpr int GPB = BM / VEC;
+      if (tid < BM) {
+        const int cg = tid / VEC, q = tid % VEC;
+        float a = 0.f, b = 0.f;
+        for (int k = 0; k < NT / GPB; ++k) {
+          a += red[(k * GPB + cg) * VEC + q];
+          b += red[NT * VEC + (k * GPB + cg) * VEC + q];
+        }
+        const int m = m0 + tid;
+        if (m < d.mdim) {
+          d.part[((int64_t)blockIdx.z * 2 + 0) * d.mdim + m] = a;
+          d.part[((int64_t)blockIdx.z * 2 + 1) * d.mdim + m] = b;
+        }
+      }
+    }
+  }
   // D[m][n]: row = g*4 + e (output channel), col = li (tile column)
   const int ncol_all = 9 * d.ndim;
   float* __restrict__ ws = d.ws + (int64_t)blockIdx.z * d.mdim * ncol_all;
@@ -234,7 +304,10 @@ Plan plan(const rdn_wgrad_desc* d) {
 template <typename T, int BM, int CK>
 int launch_w(const rdn_wgrad_desc* d, const Plan& p, hipStream_t st) {
   dim3 grid(p.mtiles, p.chunks, p.splits);
-  wgrad3_halo_kernel<T, BM, CK><<<grid, NT, 0, st>>>(*d, p.tiles_x, p.tiles_y, p.ntiles, p.tpb);
+  if (d->a_gate)
+    wgrad3_halo_kernel<T, BM, CK, true><<<grid, NT, 0, st>>>(*d, p.tiles_x, p.tiles_y, p.ntiles, p.tpb);
+  else
+    wgrad3_halo_kernel<T, BM, CK, false><<<grid, NT, 0, st>>>(*d, p.tiles_x, p.tiles_y, p.ntiles, p.tpb);
   return rdn_check_launch("rdn_conv_wgrad(conv3)");
 }
 
@@ -253,6 +326,7 @@ int launch_ck(const rdn_wgrad_desc* d, const Plan& p, hipStream_t st) {
 }  // namespace
 
 int rdn_wgrad3_splits(const rdn_wgrad_desc* d) { return plan(d).splits; }
+int rdn_wgrad3_chunks(const rdn_wgrad_desc* d) { return plan(d).chunks; }
 
 int rdn_wgrad3_launch(const rdn_wgrad_desc* d, hipStream_t st) {
   const Plan p = plan(d);

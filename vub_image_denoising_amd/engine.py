@@ -23,6 +23,7 @@ dependency order of the reference's autograd graph; see DESIGN.md.
 from __future__ import annotations
 
 import ctypes as C
+import os
 import weakref
 from dataclasses import dataclass, field
 
@@ -433,8 +434,22 @@ class UNetEngine:
     def _build_bwd(self):
         lib = H.lib()
         ws_need = 0
+        part_need = 0
         for L in self.layers:
             olvl = self._out_level(L)
+            # 3x3 convs whose output gradient arrives as an NHWC slice run the
+            # PReLU backward inside their dgrad / wgrad loaders (gate = saved
+            # PReLU input); the output conv (NCHW dy) and the 2x2 convs keep
+            # the separate rdn_prelu_bwd pass producing dYpre.
+            fused = (L.kind == "c3" and L.ddst is not None) and os.environ.get("RDN_FUSE_PRELU", "1") != "0"
+            if fused:  # only when the wgrad reads operand A once (one input-channel chunk)
+                n_, h_, w_ = self.grid[L.level]
+                probe = H.WgradDesc(dtype=self.code, gather=H.RDN_G_CONV3, n=n_, h=h_, w=w_, hin=h_, win=w_,
+                                    mdim=L.cout, ndim=L.cin_pad)
+                fused = lib.rdn_wgrad_chunks(C.byref(probe)) == 1
+            L.extra["fused"] = fused
+            pre = self.bufs[L.pre]
+            alpha = self.named[L.act + ".weight"]
             # --- input gradient (dgrad) as a forward-shaped conv over dYpre
             d = H.ConvDesc()
             d.dtype = self.code
@@ -447,6 +462,10 @@ class UNetEngine:
                 d.gather, d.hin, d.win = H.RDN_G_CONV3, h, w
                 d.x_ps, d.cin = L.cout_pad, L.cout_pad
                 d.ncols = d.cout = L.cin
+                if fused:
+                    dd = self._buf(L.ddst.buf)
+                    d.x, d.x_ps, d.x_c0 = dd.data_ptr(), dd.shape[1], L.ddst.c0
+                    d.gate, d.gate_ps, d.gate_alpha = pre.data_ptr(), pre.shape[1], alpha.data_ptr()
             elif L.kind == "down":       # per-pixel GEMM on the low-res grid, scattered to 2x2
                 n, h, w = self.grid[L.level]
                 d.gather, d.hin, d.win = H.RDN_G_PIX, h, w
@@ -479,6 +498,10 @@ class UNetEngine:
                 wg.a, wg.a_ps, wg.a_c0, wg.mdim = self.dyp.data_ptr(), L.cout_pad, 0, L.cout
                 wg.b, wg.b_ps, wg.b_c0, wg.ndim = src.data_ptr(), src.shape[1], L.src.c0, L.cin_pad
                 taps, ndim_real = 9, L.cin
+                if fused:
+                    dd = self._buf(L.ddst.buf)
+                    wg.a, wg.a_ps, wg.a_c0 = dd.data_ptr(), dd.shape[1], L.ddst.c0
+                    wg.a_gate, wg.a_gate_ps, wg.a_gate_alpha = pre.data_ptr(), pre.shape[1], alpha.data_ptr()
             elif L.kind == "down":
                 n, h, w = self.grid[L.level]
                 wg.gather, wg.n, wg.h, wg.w, wg.hin, wg.win = H.RDN_G_S2, n, h, w, 2 * h, 2 * w
@@ -497,6 +520,8 @@ class UNetEngine:
             splits = lib.rdn_wgrad_splits(C.byref(wg))
             wg.splits = splits
             ws_need = max(ws_need, lib.rdn_wgrad_workspace_size(C.byref(wg)))
+            if fused:
+                part_need = max(part_need, splits * 2 * wg.mdim * 4)
             L.wgrad_desc = wg
             L.extra["wgrad"] = (splits, wg.mdim, wg.ndim, ndim_real, taps)
             L.extra["grad_w"] = self.fp.gviews[self.fp.names.index(L.name + ".weight")]
@@ -505,8 +530,12 @@ class UNetEngine:
             L.extra["olvl"] = olvl
             L.extra["pidx"] = [self.fp.names.index(n) for n in (L.name + ".weight", L.name + ".bias", L.act + ".weight")]
         self.ws = torch.zeros(max(ws_need // 4, 4), dtype=torch.float32, device=self.device)
+        if part_need > self.pws.numel() * 4:
+            self.pws = torch.zeros(part_need // 4, dtype=torch.float32, device=self.device)
         for L in self.layers:
             L.wgrad_desc.ws = self.ws.data_ptr()
+            if L.extra["fused"]:
+                L.wgrad_desc.part = self.pws.data_ptr()
 
     def _kernel_key(self, desc):
         """Name of the kernel template instantiation a conv descriptor launches
@@ -605,7 +634,10 @@ class UNetEngine:
             P = self.P[olvl]
             pre = self.bufs[L.pre]
             ga, gb = L.extra["grad_a"], L.extra["grad_b"]
-            if L.ddst is None:
+            fused = L.extra["fused"]
+            if fused:
+                rc = 0
+            elif L.ddst is None:
                 rc = lib.rdn_prelu_bwd(self.code, P, n, h, w, L.cout, L.cout_pad, None, 0, 0, dy.data_ptr(),
                                        pre.data_ptr(), pre.shape[1], self.named[L.act + ".weight"].data_ptr(),
                                        dyp, ga.data_ptr(), gb.data_ptr(), self.pws.data_ptr(), st)
@@ -631,8 +663,13 @@ class UNetEngine:
             if rc:
                 H.check(rc, f"wgrad[{L.name}]")
             splits, mdim, ndim, ndim_real, taps = L.extra["wgrad"]
-            rc = lib.rdn_wgrad_reduce(self.ws.data_ptr(), splits, mdim, ndim, ndim_real, taps,
-                                      L.extra["grad_w"].data_ptr(), 1, st)
+            if fused:
+                rc = lib.rdn_wgrad_reduce(self.ws.data_ptr(), splits, mdim, ndim, ndim_real, taps,
+                                          L.extra["grad_w"].data_ptr(), 1, self.pws.data_ptr(), ga.data_ptr(),
+                                          gb.data_ptr(), st)
+            else:
+                rc = lib.rdn_wgrad_reduce(self.ws.data_ptr(), splits, mdim, ndim, ndim_real, taps,
+                                          L.extra["grad_w"].data_ptr(), 1, None, None, None, st)
             if rc:
                 H.check(rc, f"wgrad_reduce[{L.name}]")
             if sync is not None:
