@@ -1,0 +1,91 @@
+"""Data-parallel gradient sync (vub_image_denoising_amd/ddp.py) with world_size 2
+over gloo on the CPU: bucket planning, completion-driven launch order, averaging."""
+import os
+import socket
+import types
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from vub_image_denoising_amd.ddp import GradSync, plan_buckets
+
+
+def _fake_flat(seed, sizes):
+    g = torch.Generator().manual_seed(seed)
+    offs, o = [], 0
+    for n in sizes:
+        offs.append(o)
+        o += (n + 63) // 64 * 64
+    params = [torch.zeros(n) for n in sizes]
+    gflat = torch.zeros(o)
+    for p, off in zip(params, offs):
+        gflat[off:off + p.numel()] = torch.randn(p.numel(), generator=g)
+    return types.SimpleNamespace(params=params, offsets=offs, numel=o, gflat=gflat,
+                                 names=[f"p{i}" for i in range(len(sizes))])
+
+
+SIZES = [4608, 16, 16, 72000, 32, 32, 16, 300000, 128, 128, 5, 900000, 64]
+
+
+def test_plan_buckets_cover_everything_once():
+    fp = _fake_flat(0, SIZES)
+    b = plan_buckets(SIZES, fp.offsets, 100000)
+    covered = []
+    hi_prev = None
+    for lo, hi, first in b:
+        hi = fp.numel if hi is None else hi
+        if hi_prev is not None:
+            assert hi == hi_prev  # contiguous, filled from the end
+        covered.append((lo, hi))
+        hi_prev = lo
+    assert covered[0][1] == fp.numel and covered[-1][0] == 0
+    # a parameter larger than the bucket size gets a bucket of its own
+    assert any(hi - lo >= 900000 for lo, hi in covered)
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        fp = _fake_flat(100 + rank, SIZES)
+        mine = fp.gflat.clone()
+        gs = GradSync(fp, bucket_mb=0.4, overlap=False)
+        gs.begin()
+        # backward order: parameters complete from the last to the first, in groups of 3
+        idx = list(range(len(SIZES)))[::-1]
+        for i in range(0, len(idx), 3):
+            gs.params_done(idx[i:i + 3])
+        assert all(gs._launched), "every bucket launched once its parameters completed"
+        gs.finish()
+        q.put((rank, mine, fp.gflat.clone()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_gradsync_world2_gloo_average():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict()
+    for _ in range(2):
+        r, mine, synced = q.get(timeout=120)
+        res[r] = (mine, synced)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    avg = (res[0][0] + res[1][0]) / 2
+    torch.testing.assert_close(res[0][1], avg)
+    torch.testing.assert_close(res[1][1], avg)
