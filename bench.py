@@ -55,6 +55,18 @@ class EventTracer:
         e.record()
         self.records.append((tok[0], tok[1], e))
 
+    def per_layer(self):
+        torch.cuda.synchronize()
+        rows = {}
+        for info, s, e in self.records:
+            k = (info[1], info[0])
+            r = rows.setdefault(k, {"ms": 0.0, "n": 0, "flops": info[3], "bytes": info[4], "kernel": info[2]})
+            r["ms"] += s.elapsed_time(e)
+            r["n"] += 1
+        return [{"layer": k[0], "phase": k[1], "kernel": v["kernel"], "us": round(1e3 * v["ms"] / v["n"], 2),
+                 "tflops": round(v["flops"] / (v["ms"] / v["n"] * 1e-3) / 1e12, 1),
+                 "gbs": round(v["bytes"] / (v["ms"] / v["n"] * 1e-3) / 1e9, 1)} for k, v in rows.items()]
+
     def summary(self):
         torch.cuda.synchronize()
         by = {}
@@ -173,6 +185,8 @@ def main():
         with open(args.layer_report, "w") as f:
             json.dump({k: {kk: (sorted(vv) if isinstance(vv, set) else vv) for kk, vv in d.items()}
                        for k, d in sorted(table.items(), key=lambda kv: -kv[1]["ms"])}, f, indent=1)
+        with open(args.layer_report.replace(".json", "_per_layer.json"), "w") as f:
+            json.dump(prof.per_layer(), f, indent=0)
 
     # timed region: events only around the dominant kernel's launches
     live = EventTracer(keys={dom})

@@ -26,7 +26,15 @@ def load(path):
 # (name, N, H, W, buf_in, cin, cout_cols, kind) kind: fwd (bias+prelu+pre) | dgrad (store)
 SHAPES = [
     ("L0 conv_0 32->16", 16, 256, 256, 80, 32, 16, "fwd"),
+    ("L0 conv_1 48->16", 16, 256, 256, 80, 48, 16, "fwd"),
+    ("L0 conv_2 64->16", 16, 256, 256, 80, 64, 16, "fwd"),
     ("L0 conv_3 80->32", 16, 256, 256, 80, 80, 32, "fwd"),
+    ("L1 conv_0 64->32", 16, 128, 128, 160, 64, 32, "fwd"),
+    ("L1 conv_1 96->32", 16, 128, 128, 160, 96, 32, "fwd"),
+    ("L0 dgrad1 16->48", 16, 256, 256, 16, 16, 48, "dgrad"),
+    ("L0 dgrad2 16->64", 16, 256, 256, 16, 16, 64, "dgrad"),
+    ("L0 up0 dgrad 32->96", 16, 256, 256, 32, 32, 96, "dgrad"),
+    ("L1 dgrad0 32->64", 16, 128, 128, 32, 32, 64, "dgrad"),
     ("L0 dgrad3 32->80", 16, 256, 256, 32, 32, 80, "dgrad"),
     ("L1 conv_3 160->64", 16, 128, 128, 160, 160, 64, "fwd"),
     ("L1 dgrad3 64->160", 16, 128, 128, 64, 64, 160, "dgrad"),
@@ -71,7 +79,10 @@ def main():
     st = torch.cuda.current_stream().cuda_stream
     reps = int(os.environ.get("KB_REPS", "20"))
     print(f"{'shape':24s} " + " ".join(f"{os.path.basename(p)[:22]:>24s}" for p in libs))
+    only = os.environ.get("KB_ONLY", "")
     for shp in SHAPES:
+        if only and only not in shp[0]:
+            continue
         res = []
         setups = [setup(lib, shp, dt) for lib in L]
         times = [[] for _ in L]

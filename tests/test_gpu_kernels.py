@@ -54,6 +54,8 @@ def _seed():
 @pytest.mark.parametrize("N,Hh,Ww,Cs_in,ci0,cin,cout,Cs_out,co0", [
     (2, 16, 16, 80, 0, 48, 16, 80, 48),   # dense conv_1 of a 32-ch block: channel slice in/out
     (1, 8, 24, 32, 0, 32, 32, 32, 0),
+    (2, 16, 16, 80, 0, 80, 32, 112, 80),  # whole-row chunk (bf16 CK=80), conv_3 of level 0
+    (1, 10, 20, 96, 0, 96, 32, 128, 96),  # CK=96, ragged tiles
     (2, 8, 8, 160, 0, 160, 64, 160, 96),
     (1, 16, 16, 8, 0, 8, 32, 32, 0),      # input conv (8 padded channels)
     (3, 4, 4, 640, 0, 640, 256, 256, 0),  # deepest conv_3 shape, BN=128 with 2 N tiles
@@ -391,3 +393,57 @@ def test_fused_prelu_gate_matches_separate_pass(dt):
     assert torch.equal(o1, o2)
     assert torch.equal(g1, g2)
     assert _rel(da2, da1) < 1e-5 and _rel(db2, db1) < 1e-5
+
+
+@pytest.mark.parametrize("cin,cout,Cs_in,gate,accum", [
+    (80, 32, 80, False, False),   # level-0 conv_3 (CK=80, BN=32), residual epilogue
+    (32, 80, 32, True, True),     # its input gradient: gated dY, accumulate, BN=80 (2 epilogue passes)
+    (16, 64, 48, True, False),    # conv_2 dgrad slice of a wider gradient buffer
+    (96, 32, 96, False, False),   # up_0.conv (CK=96, one block per CU)
+    (8, 32, 8, False, False),     # input conv
+])
+def test_conv3_ws_matches_halo(cin, cout, Cs_in, gate, accum):
+    """The weight-stationary persistent kernel (default for bf16 single-chunk,
+    <= 96-column layers) against the K-streaming halo kernel (forced with an
+    explicit bn) on a multi-tile ragged image: every tile, flag and the gate
+    must give bitwise-identical results (same MFMA k order, same epilogue)."""
+    dt, code, lib, st = torch.bfloat16, H.RDN_BF16, H.lib(), H.stream_ptr()
+    N, Hh, Ww = 6, 120, 136          # 810 tiles: several tiles per persistent block
+    P = N * Hh * Ww
+    x = torch.randn(P, Cs_in, device="cuda").to(dt)
+    w = (torch.randn(cout, cin, 3, 3, device="cuda") / (3 * cin ** 0.5)).contiguous()
+    b = torch.randn(cout, device="cuda") * 0.1
+    a = torch.rand(cout, device="cuda") * 0.5
+    ga = torch.rand(cin, device="cuda")
+    pre_in = torch.randn(P, cin, device="cuda").to(dt)
+    pre_in[::3] = 0
+    res = torch.randn(P, cout, device="cuda").to(dt)
+    wp = _pack(H.PACK_CONV_FWD, w, cout, cin, 3, 3, 0, cin, cout, 9 * cin, dt)
+    init = torch.randn(P, cout, device="cuda").to(dt)
+    outs = []
+    for bn in (0, 16):
+        out, pre = init.clone(), torch.zeros(P, cout, dtype=dt, device="cuda")
+        flags = H.EPI_ACCUM if accum else (H.EPI_BIAS | H.EPI_PRELU | H.EPI_STORE_PRE | H.EPI_RESID)
+        d = H.ConvDesc(dtype=code, gather=H.RDN_G_CONV3, flags=flags, n=N, h=Hh, w=Ww, hin=Hh, win=Ww, cin=cin,
+                       x=x.data_ptr(), x_ps=Cs_in, x_c0=Cs_in - cin, wp=wp.data_ptr(), kp=wp.shape[1], ncols=cout,
+                       cout=cout, bias=b.data_ptr(), alpha=a.data_ptr(), out=out.data_ptr(), out_ps=cout, out_c0=0,
+                       pre=pre.data_ptr(), pre_ps=cout, res=res.data_ptr(), res_ps=cout, res_c0=0, res_climit=cout,
+                       bn=bn)
+        if gate:
+            d.gate, d.gate_ps, d.gate_alpha = pre_in.data_ptr(), cin, ga.data_ptr()
+        H.check(lib.rdn_conv_fwd(C.byref(d), st))
+        outs.append((out, pre))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+    # and against torch on one image
+    xs = _nchw(x, N, Hh, Ww, Cs_in - cin, cin)[:1]
+    if gate:
+        ps = _nchw(pre_in, N, Hh, Ww, 0, cin)[:1]
+        xs = torch.where(ps > 0, xs, ga.cpu().view(1, -1, 1, 1) * xs).to(dt).float()
+    ref = F.conv2d(xs, w.cpu().to(dt).float(), None if accum else b.cpu(), padding=1)
+    if accum:
+        ref = ref + _nchw(init, N, Hh, Ww, 0, cout)[:1]
+    else:
+        ref = F.prelu(ref, a.cpu()) + _nchw(res, N, Hh, Ww, 0, cout)[:1]
+    assert _rel(_nchw(outs[0][0], N, Hh, Ww, 0, cout)[:1], ref) < 2e-2

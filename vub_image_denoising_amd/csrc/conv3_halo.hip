@@ -16,16 +16,17 @@
 //
 // Packed weight layout (rdn_pack_weights with ck > 0):
 //   P[n][chunk*KC + tap*CK + ci],  KC = roundup(9*CK, SK),  SK = 128 B / elem.
-#include "rdn_common.h"
+#include "conv3_tile.h"
 
 namespace {
 
 constexpr int NT = 256;
-constexpr int TH = 8, TW = 16, BM = TH * TW;
-constexpr int HW_ = (TH + 2) * (TW + 2);   // halo pixels
+using c3::TH;
+using c3::TW;
+using c3::BM;
+using c3::HW_;
+using c3::HaloRow;
 constexpr int ROWB = 160;                  // B-stage row: 128 B + 32 B pad (conflict-free ds_read_b128)
-
-template <int CKB> struct HaloRow { static constexpr int V = CKB >= 64 ? CKB + 32 : CKB; };
 
 // occupancy request: narrow tiles keep 2 waves/SIMD, wide tiles let the
 // register allocator use up to 512 VGPRs (measured faster: scripts/kbench.py)
@@ -75,7 +76,7 @@ __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_
   // ---- halo loader: unit u -> (halo pixel, 16-B channel group).  With GATE
   // the unit is dY and becomes dYpre = dY * (pre > 0 ? 1 : alpha) when it is
   // written to LDS (PReLU backward fused into the input-gradient conv).
-  static_assert(NT % HU == 0, "fixed channel group per thread");
+  static_assert(!GATE || NT % HU == 0, "fixed channel group per thread");
   u32x4 hreg[H_IT];
   u32x4 greg[GATE ? H_IT : 1];
   float galpha[GATE ? VEC : 1];
@@ -267,92 +268,23 @@ __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_
         Ct[((wm * WTM + i * 16 + g * 4 + e) * CROW) / 4 + wn * WTN + jn * 16 + r] = acc[i][jn][e];
   __syncthreads();
 
-  const int flags = d.flags;
-  T* __restrict__ OUT = (T*)d.out;
-  T* __restrict__ PRE = (T*)d.pre;
-  const T* __restrict__ RES = (const T*)d.res;
-  constexpr int UPR = BN / VEC;         // 16-B units per tile row
-  constexpr int E_UNITS = BM * UPR;
-  for (int u = tid; u < E_UNITS; u += NT) {
-    const int p = u / UPR, cu = u - p * UPR;
-    const int yy = y0 + p / TW, xx = x0 + p % TW;
-    const int c = n0 + cu * VEC;
-    if (yy >= H || xx >= W || c >= d.ncols) continue;
-    const int64_t opix = ((int64_t)nimg * H + yy) * W + xx;
-    float v[VEC];
-    {
-      const float* src = Ct + (p * CROW) / 4 + cu * VEC;
-#pragma unroll
-      for (int q = 0; q < VEC; q += 4) {
-        const f32x4 t4 = *(const f32x4*)(src + q);
-        v[q] = t4[0]; v[q + 1] = t4[1]; v[q + 2] = t4[2]; v[q + 3] = t4[3];
-      }
-    }
-    const bool full = c + VEC <= d.ncols;
-    if (flags & RDN_EPI_BIAS) {
-#pragma unroll
-      for (int q = 0; q < VEC; ++q) v[q] += (c + q < d.ncols) ? d.bias[c + q] : 0.f;
-    }
-    if (flags & RDN_EPI_STORE_PRE) {
-      T* pp = PRE + opix * d.pre_ps + c;
-      if (full) *(u32x4*)pp = Unit16<T>::pack(v);
-      else
-        for (int q = 0; q < VEC && c + q < d.ncols; ++q) pp[q] = from_f32<T>(v[q]);
-    }
-    if (flags & RDN_EPI_PRELU) {
-#pragma unroll
-      for (int q = 0; q < VEC; ++q) {
-        const float a = (c + q < d.ncols) ? d.alpha[c + q] : 0.f;
-        v[q] = v[q] > 0.f ? v[q] : a * v[q];
-      }
-    }
-    if (flags & RDN_EPI_OUT_NCHW) {
-      for (int q = 0; q < VEC && c + q < d.ncols; ++q) {
-        const int64_t o = (((int64_t)nimg * d.cout + c + q) * H + yy) * W + xx;
-        float w = v[q];
-        if (flags & RDN_EPI_RESID) w += d.res_nchw[o];
-        if (flags & RDN_EPI_ACCUM) w += d.out_nchw[o];
-        d.out_nchw[o] = w;
-      }
-      continue;
-    }
-    if (flags & RDN_EPI_RESID) {
-      const T* rp = RES + opix * d.res_ps + d.res_c0 + c;
-      if (full && c + VEC <= d.res_climit) {
-        float rv[VEC];
-        Unit16<T>::unpack(*(const u32x4*)rp, rv);
-#pragma unroll
-        for (int q = 0; q < VEC; ++q) v[q] += rv[q];
-      } else {
-        for (int q = 0; q < VEC; ++q)
-          if (c + q < d.res_climit && c + q < d.ncols) v[q] += to_f32(rp[q]);
-      }
-    }
-    T* op = OUT + opix * d.out_ps + d.out_c0 + c;
-    if (full) {
-      if (flags & RDN_EPI_ACCUM) {
-        float ov[VEC];
-        Unit16<T>::unpack(*(const u32x4*)op, ov);
-#pragma unroll
-        for (int q = 0; q < VEC; ++q) v[q] += ov[q];
-      }
-      *(u32x4*)op = Unit16<T>::pack(v);
-    } else {
-      for (int q = 0; q < VEC && c + q < d.ncols; ++q) {
-        float w = v[q];
-        if (flags & RDN_EPI_ACCUM) w += to_f32(op[q]);
-        op[q] = from_f32<T>(w);
-      }
-    }
-  }
+  c3::store_tile<T, BN, NT>(d, Ct, CROW / 4, y0, x0, nimg, n0, tid);
 }
 
 template <typename T, int BN, int WMW, int CK>
 int launch_h(const rdn_conv_desc* d, hipStream_t st) {
   const int tiles_x = (d->w + TW - 1) / TW, tiles_y = (d->h + TH - 1) / TH;
   dim3 grid((unsigned)(d->n * tiles_x * tiles_y), (unsigned)((d->ncols + BN - 1) / BN));
-  if (d->gate) conv3_halo_kernel<T, BN, WMW, CK, true><<<grid, NT, 0, st>>>(*d, tiles_x, tiles_y);
-  else conv3_halo_kernel<T, BN, WMW, CK, false><<<grid, NT, 0, st>>>(*d, tiles_x, tiles_y);
+  if (d->gate) {
+    if constexpr (NT % (CK / TypeInfo<T>::VEC) == 0)
+      conv3_halo_kernel<T, BN, WMW, CK, true><<<grid, NT, 0, st>>>(*d, tiles_x, tiles_y);
+    else {
+      rdn_set_error("rdn_conv_fwd(conv3): gated input needs a power-of-two channel chunk");
+      return RDN_E_SHAPE;
+    }
+  } else {
+    conv3_halo_kernel<T, BN, WMW, CK, false><<<grid, NT, 0, st>>>(*d, tiles_x, tiles_y);
+  }
   return rdn_check_launch("rdn_conv_fwd(conv3)");
 }
 
@@ -388,11 +320,21 @@ int launch_bn(const rdn_conv_desc* d, hipStream_t st) {
 
 }  // namespace
 
-int rdn_conv3_chunk_impl(int cin, int dtype) {
-  const int cap = dtype == RDN_BF16 ? 64 : 32;
+int rdn_conv3_chunk_pow2(int cin, int cap) {
   int ck = cap;
   while (ck > 8 && (cin % ck)) ck >>= 1;
   return (cin % ck) ? -1 : ck;
+}
+
+// K-side channel chunk of the halo conv: the whole pixel row for the narrow
+// 48/80/96-channel inputs of level 0 (bf16: one contiguous 96-192 B read per
+// pixel instead of 3-6 passes of 32 B), else the largest power of two <= 64 (bf16)
+// / 32 (fp32) dividing cin.
+int rdn_conv3_chunk_impl(int cin, int dtype) {
+#ifndef RDN_NO_WIDE_CK
+  if (dtype == RDN_BF16 && (cin == 48 || cin == 80 || cin == 96)) return cin;
+#endif
+  return rdn_conv3_chunk_pow2(cin, dtype == RDN_BF16 ? 64 : 32);
 }
 
 extern "C" int rdn_conv3_chunk(int32_t cin, int32_t dtype) { return rdn_conv3_chunk_impl(cin, dtype); }
@@ -420,7 +362,12 @@ int rdn_conv3_launch(const rdn_conv_desc* d, hipStream_t st) {
     return RDN_E_SHAPE;
   }
   if (d->dtype == RDN_BF16) {
+    const int ws = rdn_conv3_ws_launch(d, ck, st);
+    if (ws <= 0) return ws;
     switch (ck) {
+      case 96: return launch_bn<bf16, 96>(d, st);
+      case 80: return launch_bn<bf16, 80>(d, st);
+      case 48: return launch_bn<bf16, 48>(d, st);
       case 64: return launch_bn<bf16, 64>(d, st);
       case 32: return launch_bn<bf16, 32>(d, st);
       case 16: return launch_bn<bf16, 16>(d, st);

@@ -1,0 +1,451 @@
+// Weight-stationary, persistent 3x3 / pad 1 convolution for the narrow layers
+// (bf16, input channels <= 96 in ONE chunk, output columns <= 96): level 0 of
+// the network at 256x256 (Unet_model.py:48-49,60-61,72-75 forward, and the
+// input gradients of the same convs).  These layers move 100-300 MB per launch
+// and carry little arithmetic, so the limit is HBM latency hiding, not MFMA.
+//
+// conv3_halo.hip streams the weights through LDS one 128-B K stage at a time
+// (a barrier and an L2 round trip per stage: 5-15 dependent round trips per
+// 8x16 tile at these shapes).  Here the block's whole packed weight panel
+// (BN x KC bf16, <= ~64 KB) is loaded into LDS ONCE, and the block then loops
+// over output tiles (persistent grid of 1-2 blocks per CU):
+//
+//   halo(t) in LDS --> 9 taps x MFMA  (no barriers inside the K loop)
+//   halo(t+1) global loads in flight in registers meanwhile
+//   epilogue of t (fp32 tile staged in LDS, 16-B NHWC stores), then halo(t+1) -> LDS
+//
+// Work split (XCD-aware): block b runs on XCD b % 8 (round-robin dispatch);
+// XCD x owns tiles [x*T/8, (x+1)*T/8), its blocks take consecutive tiles of
+// that range in lock step, so the tiles in flight on one XCD are adjacent and
+// their overlapping halos are read through the same L2.
+//
+// Same packed layout and epilogue flags as conv3_halo (P[n][tap*CK + ci], KC =
+// roundup(9*CK, 64)); GATE = PReLU backward fused into the halo loader.
+#include "conv3_tile.h"
+
+#include <stdlib.h>
+
+namespace {
+
+constexpr int NT = 256;
+using c3::BM;
+using c3::HW_;
+using c3::TH;
+using c3::TW;
+
+constexpr int LDS_2BLK = 80 * 1024;     // two resident blocks per CU below this
+constexpr int LDS_MAX = 160 * 1024;
+
+template <int BN, int CK>
+struct WsCfg {
+  static constexpr int SK = 64;                          // k per 128-B stage
+  static constexpr int KC = (9 * CK + SK - 1) / SK * SK;
+  static constexpr int NSTG = KC / SK;
+  static constexpr int WROW = KC * 2 + 32;               // bytes, = 32 mod 128: conflict-free B reads
+  static constexpr int W_BYTES = BN * WROW;
+  static constexpr int HROW = c3::HaloRow<CK * 2>::V;
+  static constexpr int HALO_BYTES = HW_ * HROW;
+  static constexpr int NTL = BN / 16;
+  static constexpr int epi_bytes(int ntp) { return BM * (ntp * 64 + 16); }
+  static constexpr int mx(int a, int b) { return a > b ? a : b; }
+  // epilogue column passes: as wide as fits beside the weights in two-block LDS
+  static constexpr int pick_ntp() {
+    for (int t = NTL; t >= 1; --t)
+      if (W_BYTES + mx(HALO_BYTES, epi_bytes(t)) <= LDS_2BLK) return t;
+    for (int t = NTL; t > 1; --t)   // one block per CU anyway: widest pass that fits
+      if (W_BYTES + mx(HALO_BYTES, epi_bytes(t)) <= LDS_MAX) return t;
+    return 1;
+  }
+  static constexpr int NTP = pick_ntp();
+  static constexpr int NPASS = (NTL + NTP - 1) / NTP;
+  static constexpr int R2 = mx(HALO_BYTES, epi_bytes(NTP));
+  static constexpr int LDS = W_BYTES + R2;
+  static constexpr bool FITS = LDS <= LDS_MAX && NPASS <= 2;
+  static constexpr int BLK_PER_CU = LDS <= LDS_2BLK ? 2 : 1;
+};
+
+template <int BN, int CK, bool GATE>
+__global__ __launch_bounds__(NT, 2) void conv3_ws_kernel(rdn_conv_desc d, int tiles_x, int tiles_y, int ntiles) {
+  using Cfg = WsCfg<BN, CK>;
+  constexpr int VEC = 8;
+  constexpr int KC = Cfg::KC, WROW = Cfg::WROW, HROW = Cfg::HROW;
+  constexpr int NSTEP = KC / 32;                         // MFMA k-steps of 32
+  constexpr int NTL = Cfg::NTL, NTP = Cfg::NTP, NPASS = Cfg::NPASS;
+  constexpr int MT = 2;                                  // 4 waves x 32 tile pixels
+  constexpr int HU = CK / VEC;                           // 16-B units per halo pixel
+  constexpr int H_UNITS = HW_ * HU;
+  constexpr int H_IT = (H_UNITS + NT - 1) / NT;
+  constexpr int CROW_F = NTP * 16 + 4;                   // epilogue fp32 row (floats)
+  constexpr int UPR = BN / VEC;                          // 16-B output units per pixel
+  constexpr int EU = BM * UPR;
+  constexpr int E_IT = (EU + NT - 1) / NT;
+  constexpr bool COLFIX = NT % UPR == 0;                 // a thread's output channels are tile-invariant
+  constexpr bool KALIGN = CK % 32 == 0;                  // a k-step never straddles a tap
+  constexpr bool PF = E_IT <= 4;                         // epilogue operand prefetch (register budget)
+  static_assert(!GATE || NT % HU == 0, "fixed channel group per thread");
+  static_assert(Cfg::FITS, "LDS");
+
+  __shared__ __attribute__((aligned(16))) unsigned char lds[Cfg::LDS];
+  unsigned char* const wl = lds;
+  unsigned char* const halo = lds + Cfg::W_BYTES;
+  float* const Ct = (float*)(lds + Cfg::W_BYTES);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int H = d.h, W = d.w;
+
+  // this block's tiles: XCD share [t_lo, t_hi), strided by the XCD's block count
+  const int per = gridDim.x >> 3;
+  const int xcd = blockIdx.x & 7;
+  const int t_hi = (int)((int64_t)ntiles * (xcd + 1) / 8);
+  int t = (int)((int64_t)ntiles * xcd / 8) + (blockIdx.x >> 3);
+  if (t >= t_hi) return;
+
+  const bf16* __restrict__ X = (const bf16*)d.x;
+  const bf16* __restrict__ G = (const bf16*)d.gate;
+
+  // ---- resident weights: BN rows x KC, one load per block
+  {
+    const bf16* __restrict__ WP = (const bf16*)d.wp;
+    constexpr int UPRW = KC / VEC;
+    for (int u = tid; u < BN * UPRW; u += NT) {
+      const int n = u / UPRW, k8 = u - n * UPRW;
+      *(u32x4*)(wl + n * WROW + k8 * 16) = *(const u32x4*)(WP + (int64_t)n * d.kp + k8 * VEC);
+    }
+  }
+
+  // ---- tile-invariant per-thread geometry, computed once: every address below is
+  // a per-tile uniform base plus one of these offsets (no per-tile index math)
+  int hrel[H_IT], grel[GATE ? H_IT : 1], hlds[H_IT];
+#pragma unroll
+  for (int it = 0; it < H_IT; ++it) {
+    const int u = tid + it * NT;
+    const int hp = u / HU, cu = u - hp * HU;
+    const int hy = hp / (TW + 2), hx = hp - hy * (TW + 2);
+    hrel[it] = (hy * W + hx) * d.x_ps + cu * VEC;
+    if constexpr (GATE) grel[it] = (hy * W + hx) * d.gate_ps + cu * VEC;
+    hlds[it] = hp * HROW + cu * 16;
+  }
+  // A-operand LDS offsets per k-step (lane group g covers k = 32 j + 8 g .. +7):
+  // immediates when CK is a multiple of 32, else one register per k-step
+  const int a_lane = ((wave * MT) * (TW + 2) + r) * HROW;
+  int offA[KALIGN ? 1 : NSTEP];
+  if constexpr (!KALIGN) {
+#pragma unroll
+    for (int j = 0; j < NSTEP; ++j) {
+      const int k = 32 * j + 8 * g;
+      int tap = k / CK;
+      const int ci = k - tap * CK;
+      tap = tap < 9 ? tap : 8;   // padded k: zero weights, finite operand
+      offA[j] = a_lane + ((tap / 3) * (TW + 2) + tap % 3) * HROW + ci * 2;
+    }
+  }
+  const unsigned char* const pa = halo + (KALIGN ? a_lane + g * 16 : 0);
+  const unsigned char* const pb = wl + r * WROW + g * 16;
+
+  // output units of this thread: pixel offset within the tile (NHWC pixel index
+  // relative to the tile origin) and channel
+  int erel[E_IT], ecol[COLFIX ? 1 : E_IT];
+#pragma unroll
+  for (int it = 0; it < E_IT; ++it) {
+    const int u = tid + it * NT;
+    const int px = u / UPR;
+    erel[it] = (px / TW) * W + px % TW;
+    if constexpr (!COLFIX) ecol[it] = (u - px * UPR) * VEC;
+  }
+  if constexpr (COLFIX) ecol[0] = (tid % UPR) * VEC;
+  auto col_of = [&](int it) { return COLFIX ? ecol[0] : ecol[it]; };
+
+  const int flags = d.flags;
+  // fast epilogue: whole 16-B NHWC units, no NCHW output
+  const bool fast_epi = (d.ncols % VEC) == 0 && !(flags & RDN_EPI_OUT_NCHW) &&
+                        (!(flags & RDN_EPI_RESID) || (d.res_climit >= d.ncols && d.res_ps % VEC == 0 &&
+                                                      d.res_c0 % VEC == 0)) &&
+                        d.out_ps % VEC == 0 && d.out_c0 % VEC == 0 && d.pre_ps % VEC == 0;
+  float ebias[COLFIX ? VEC : 1], ealpha[COLFIX ? VEC : 1];
+  if constexpr (COLFIX) {
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) {
+      const int c = ecol[0] + q;
+      ebias[q] = ((flags & RDN_EPI_BIAS) && c < d.ncols) ? d.bias[c] : 0.f;
+      ealpha[q] = ((flags & RDN_EPI_PRELU) && c < d.ncols) ? d.alpha[c] : 0.f;
+    }
+  }
+
+  float galpha[GATE ? VEC : 1];
+  if constexpr (GATE) {
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) galpha[q] = d.gate_alpha[(tid % HU) * VEC + q];
+  }
+
+  u32x4 hreg[H_IT];
+  u32x4 greg[GATE ? H_IT : 1];
+  int y0, x0, nimg;
+  auto origin = [&](int tt, int& oy, int& ox, int& on) {
+    const int tx = tt % tiles_x;
+    tt /= tiles_x;
+    oy = (tt % tiles_y) * TH;
+    ox = tx * TW;
+    on = tt / tiles_y;
+  };
+  auto load_halo = [&](int oy, int ox, int on) {
+    const int64_t hpix0 = ((int64_t)on * H + (oy - 1)) * W + (ox - 1);   // halo pixel (0, 0)
+    const bf16* const xb = X + hpix0 * d.x_ps + d.x_c0;
+    const bf16* const gb = GATE ? G + hpix0 * d.gate_ps : nullptr;
+    const bool interior = oy >= 1 && oy + TH + 1 <= H && ox >= 1 && ox + TW + 1 <= W;
+#pragma unroll
+    for (int it = 0; it < H_IT; ++it) {
+      const int u = tid + it * NT;
+      bool ok = (it + 1 < H_IT) || u < H_UNITS;
+      if (!interior) {
+        const int hp = u / HU;
+        const int hy = hp / (TW + 2), hx = hp - hy * (TW + 2);
+        ok = ok && (unsigned)(oy - 1 + hy) < (unsigned)H && (unsigned)(ox - 1 + hx) < (unsigned)W;
+      }
+      u32x4 v = {0u, 0u, 0u, 0u}, gv = {0u, 0u, 0u, 0u};
+      if (ok) {
+        v = *(const u32x4*)(xb + hrel[it]);
+        if constexpr (GATE) gv = *(const u32x4*)(gb + grel[it]);
+      }
+      hreg[it] = v;
+      if constexpr (GATE) greg[it] = gv;
+    }
+  };
+  auto store_halo = [&]() {
+#pragma unroll
+    for (int it = 0; it < H_IT; ++it) {
+      if (it + 1 == H_IT && tid + it * NT >= H_UNITS) continue;
+      u32x4 v = hreg[it];
+      if constexpr (GATE) {
+        float dy[VEC], pr[VEC];
+        Unit16<bf16>::unpack(v, dy);
+        Unit16<bf16>::unpack(greg[it], pr);
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) dy[q] = pr[q] > 0.f ? dy[q] : galpha[q] * dy[q];
+        v = Unit16<bf16>::pack(dy);
+      }
+      *(u32x4*)(halo + hlds[it]) = v;
+    }
+  };
+
+  // epilogue read operand of a tile (residual, else the output it accumulates
+  // into), loaded one tile ahead so the epilogue does not wait on a load issued
+  // behind its own stores (fast epilogue, full tiles only)
+  const bool pf_res = PF && fast_epi && (flags & RDN_EPI_RESID);
+  const bool pf_acc = PF && fast_epi && !pf_res && (flags & RDN_EPI_ACCUM);
+  u32x4 eop[PF ? E_IT : 1];
+  auto load_epi = [&](int oy, int ox, int on) {
+    if constexpr (!PF) return;
+    if (!(pf_res || pf_acc) || oy + TH > H || ox + TW > W) return;
+    const int64_t opix0 = ((int64_t)on * H + oy) * W + ox;
+    const bf16* const base = pf_res ? (const bf16*)d.res + opix0 * d.res_ps + d.res_c0
+                                    : (const bf16*)d.out + opix0 * d.out_ps + d.out_c0;
+    const int ps = pf_res ? d.res_ps : d.out_ps;
+#pragma unroll
+    for (int it = 0; it < E_IT; ++it) {
+      if (it + 1 == E_IT && tid + it * NT >= EU) continue;
+      if (!COLFIX || col_of(it) < d.ncols) eop[it] = *(const u32x4*)(base + erel[it] * ps + col_of(it));
+    }
+  };
+
+  origin(t, y0, x0, nimg);
+  load_halo(y0, x0, nimg);
+  load_epi(y0, x0, nimg);
+  store_halo();
+  __syncthreads();
+
+  while (true) {
+    const int tn = t + per;
+    const bool has_next = tn < t_hi;
+    int ny0 = 0, nx0 = 0, nn = 0;
+    if (has_next) {
+      origin(tn, ny0, nx0, nn);
+      load_halo(ny0, nx0, nn);   // in flight during this tile's MFMAs and epilogue
+    }
+
+    f32x4 acc[MT][NTL];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int jn = 0; jn < NTL; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+    for (int j = 0; j < NSTEP; ++j) {
+      u32x4 af[MT], bfr[NTL];
+      int ao;
+      if constexpr (KALIGN) {
+        const int k0 = 32 * j;
+        int tap = k0 / CK;
+        const int ci = k0 - tap * CK;
+        tap = tap < 9 ? tap : 8;
+        ao = ((tap / 3) * (TW + 2) + tap % 3) * HROW + ci * 2;
+      } else {
+        ao = offA[j];
+      }
+#pragma unroll
+      for (int i = 0; i < MT; ++i) af[i] = *(const u32x4*)(pa + ao + i * (TW + 2) * HROW);
+#pragma unroll
+      for (int jn = 0; jn < NTL; ++jn) bfr[jn] = *(const u32x4*)(pb + jn * 16 * WROW + j * 64);
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int jn = 0; jn < NTL; ++jn)
+          acc[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[i]),
+                                                               __builtin_bit_cast(bf16x8, bfr[jn]), acc[i][jn], 0, 0,
+                                                               0);
+    }
+    __syncthreads();   // halo reads done: Ct aliases it
+
+    const bool full_tile = y0 + TH <= H && x0 + TW <= W;
+    const int64_t opix0 = ((int64_t)nimg * H + y0) * W + x0;
+#pragma unroll
+    for (int p = 0; p < NPASS; ++p) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int jn = p * NTP; jn < (p + 1) * NTP && jn < NTL; ++jn)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            Ct[(wave * 32 + i * 16 + g * 4 + e) * CROW_F + (jn - p * NTP) * 16 + r] = acc[i][jn][e];
+      __syncthreads();
+      if (fast_epi && full_tile) {
+#pragma unroll
+        for (int it = 0; it < E_IT; ++it) {
+          const int u = tid + it * NT;
+          const int c = col_of(it);
+          if ((it + 1 == E_IT && u >= EU) || c < p * NTP * 16 || c >= (p + 1) * NTP * 16 || c >= d.ncols) continue;
+          const int px = u / UPR;
+          float v[VEC];
+          const float* src = Ct + px * CROW_F + c - p * NTP * 16;
+#pragma unroll
+          for (int q = 0; q < VEC; q += 4) {
+            const f32x4 t4 = *(const f32x4*)(src + q);
+            v[q] = t4[0]; v[q + 1] = t4[1]; v[q + 2] = t4[2]; v[q + 3] = t4[3];
+          }
+          const int64_t opix = opix0 + erel[it];
+          if (flags & RDN_EPI_BIAS) {
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) v[q] += COLFIX ? ebias[q] : d.bias[c + q];
+          }
+          if (flags & RDN_EPI_STORE_PRE) *(u32x4*)((bf16*)d.pre + opix * d.pre_ps + c) = Unit16<bf16>::pack(v);
+          if (flags & RDN_EPI_PRELU) {
+#pragma unroll
+            for (int q = 0; q < VEC; ++q) {
+              const float a = COLFIX ? ealpha[q] : d.alpha[c + q];
+              v[q] = v[q] > 0.f ? v[q] : a * v[q];
+            }
+          }
+          bf16* const op = (bf16*)d.out + opix * d.out_ps + d.out_c0 + c;
+          if (flags & (RDN_EPI_RESID | RDN_EPI_ACCUM)) {
+            float rv[VEC];
+            if (flags & RDN_EPI_RESID) {
+              Unit16<bf16>::unpack(pf_res ? eop[PF ? it : 0]
+                                          : *(const u32x4*)((const bf16*)d.res + opix * d.res_ps + d.res_c0 + c),
+                                   rv);
+#pragma unroll
+              for (int q = 0; q < VEC; ++q) v[q] += rv[q];
+            }
+            if (flags & RDN_EPI_ACCUM) {
+              Unit16<bf16>::unpack(pf_acc ? eop[PF ? it : 0] : *(const u32x4*)op, rv);
+#pragma unroll
+              for (int q = 0; q < VEC; ++q) v[q] += rv[q];
+            }
+          }
+          *(u32x4*)op = Unit16<bf16>::pack(v);
+        }
+      } else {
+        // ragged tile / partial units / NCHW output: generic per-unit epilogue
+        c3::store_tile<bf16, NTP * 16, NT>(d, Ct, CROW_F, y0, x0, nimg, p * NTP * 16, tid);
+      }
+      __syncthreads();
+    }
+
+    if (!has_next) break;
+    load_epi(ny0, nx0, nn);   // in flight during the next tile's MFMAs
+    store_halo();
+    __syncthreads();
+    t = tn;
+    y0 = ny0;
+    x0 = nx0;
+    nimg = nn;
+  }
+}
+
+int ws_enabled() {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = getenv("RDN_CONV3_WS");
+    on = (e && e[0] == '0') ? 0 : 1;
+  }
+  return on;
+}
+
+template <int BN, int CK>
+int launch_ws(const rdn_conv_desc* d, hipStream_t st) {
+  using Cfg = WsCfg<BN, CK>;
+  if constexpr (!Cfg::FITS) {
+    return 1;
+  } else {
+    const int tiles_x = (d->w + TW - 1) / TW, tiles_y = (d->h + TH - 1) / TH;
+    const int64_t nt = (int64_t)d->n * tiles_x * tiles_y;
+    if (nt >= (1ll << 31)) return 1;
+    const int ntiles = (int)nt;
+    int dev = 0, cus = 256;
+    (void)hipGetDevice(&dev);
+    static int cached_cus = 0;
+    if (!cached_cus) {
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+      cached_cus = cus;
+    }
+    cus = cached_cus;
+    const int per_xcd = (ntiles + 7) / 8;
+    int slots = cus * Cfg::BLK_PER_CU / 8;
+    if (slots > per_xcd) slots = per_xcd;
+    if (slots < 1) slots = 1;
+    dim3 grid((unsigned)(8 * slots));
+    constexpr int HU = CK / 8;
+    if (d->gate) {
+      if constexpr (NT % HU == 0)
+        conv3_ws_kernel<BN, CK, true><<<grid, NT, 0, st>>>(*d, tiles_x, tiles_y, ntiles);
+      else
+        return 1;
+    } else {
+      conv3_ws_kernel<BN, CK, false><<<grid, NT, 0, st>>>(*d, tiles_x, tiles_y, ntiles);
+    }
+    return rdn_check_launch("rdn_conv_fwd(conv3 ws)");
+  }
+}
+
+template <int CK>
+int ws_bn(const rdn_conv_desc* d, hipStream_t st) {
+  switch ((d->ncols + 15) / 16) {
+    case 1: return launch_ws<16, CK>(d, st);
+    case 2: return launch_ws<32, CK>(d, st);
+    case 3: return launch_ws<48, CK>(d, st);
+    case 4: return launch_ws<64, CK>(d, st);
+    case 5: return launch_ws<80, CK>(d, st);
+    case 6: return launch_ws<96, CK>(d, st);
+  }
+  return 1;
+}
+
+}  // namespace
+
+// 0 = launched, < 0 = error, 1 = shape not served here (caller uses conv3_halo)
+int rdn_conv3_ws_launch(const rdn_conv_desc* d, int ck, hipStream_t st) {
+#ifdef RDN_NO_WS
+  return 1;
+#endif
+  if (!ws_enabled() || d->dtype != RDN_BF16 || d->bn || ck != d->cin || d->ncols > 96) return 1;
+  if (d->x_ps % 8 || d->x_c0 % 8 || ((uintptr_t)d->x & 15) || ((uintptr_t)d->wp & 15) || d->kp % 8) return 1;
+  switch (ck) {
+    case 8: return ws_bn<8>(d, st);
+    case 16: return ws_bn<16>(d, st);
+    case 32: return ws_bn<32>(d, st);
+    case 48: return ws_bn<48>(d, st);
+    case 64: return ws_bn<64>(d, st);
+    case 80: return ws_bn<80>(d, st);
+    case 96: return ws_bn<96>(d, st);
+  }
+  return 1;
+}

@@ -282,7 +282,7 @@ struct Plan { int bm, ck, mtiles, chunks, tiles_x, tiles_y, ntiles, tpb, splits;
 Plan plan(const rdn_wgrad_desc* d) {
   Plan p;
   p.bm = d->mdim <= 16 ? 16 : d->mdim <= 32 ? 32 : 64;
-  int ck = rdn_conv3_chunk_impl(d->ndim, d->dtype);
+  int ck = rdn_conv3_chunk_pow2(d->ndim, d->dtype == RDN_BF16 ? 64 : 32);
   const int cap = d->dtype == RDN_BF16 ? (p.bm <= 32 ? 64 : 32) : 32;
   while (ck > cap) ck >>= 1;
   p.ck = ck;

@@ -554,9 +554,9 @@ class UNetEngine:
         dt = "bf16" if self.code == H.RDN_BF16 else "f32"
         if wg.gather == H.RDN_G_CONV3:
             bm = 16 if wg.mdim <= 16 else 32 if wg.mdim <= 32 else 64
-            ck = H.lib().rdn_conv3_chunk(wg.ndim, self.code)
             cap = (64 if bm <= 32 else 32) if self.code == H.RDN_BF16 else 32
-            while ck > cap:
+            ck = cap
+            while ck > 8 and wg.ndim % ck:
                 ck //= 2
             return f"wgrad3_halo_kernel<{dt},{bm},{ck}>"
         bm = 16 if wg.mdim <= 16 else 32 if wg.mdim <= 32 else 64
