@@ -89,6 +89,9 @@ typedef struct rdn_conv_desc {
 
 /* Implicit-GEMM convolution (MFMA) with the fused epilogue above. */
 int rdn_conv_fwd(const rdn_conv_desc* d, void* stream);
+/* name of the kernel instantiation rdn_conv_fwd would launch for d (nothing is
+   launched); for profiles and per-kernel timing */
+int rdn_conv_kernel_name(const rdn_conv_desc* d, char* buf, int32_t len);
 
 typedef struct rdn_wgrad_desc {
   int32_t dtype, gather;   /* gather of the B operand: RDN_G_CONV3 or RDN_G_S2 */
@@ -108,6 +111,8 @@ typedef struct rdn_wgrad_desc {
 
 /* dW[m][tap][nd] partials = sum over pixels p of A[p][m] * B[gather(p,tap)][nd] */
 int rdn_conv_wgrad(const rdn_wgrad_desc* d, void* stream);
+/* name of the kernel instantiation rdn_conv_wgrad would launch for d */
+int rdn_wgrad_kernel_name(const rdn_wgrad_desc* d, char* buf, int32_t len);
 /* split count the automatic mode would use, and the workspace it needs (bytes) */
 int rdn_wgrad_splits(const rdn_wgrad_desc* d);
 /* input-channel chunks (grid.y) of the 3x3 weight-gradient kernel: operand A is

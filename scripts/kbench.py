@@ -72,6 +72,73 @@ def setup(lib, shp, dt):
     return d, (x, w, wp, b, a, out, pre), flops, byts
 
 
+# weight gradients: (name, N, H, W, a_ps, mdim, b_ps, ndim)
+WSHAPES = [
+    ("L0 wgrad conv_0 16x32", 16, 256, 256, 16, 16, 80, 32),
+    ("L0 wgrad conv_1 16x48", 16, 256, 256, 16, 16, 80, 48),
+    ("L0 wgrad conv_3 32x80", 16, 256, 256, 32, 32, 80, 80),
+    ("L0 wgrad up0 32x96", 16, 256, 256, 32, 32, 96, 96),
+    ("L1 wgrad conv_0 32x64", 16, 128, 128, 32, 32, 160, 64),
+    ("L1 wgrad conv_3 64x160", 16, 128, 128, 64, 64, 160, 160),
+    ("L2 wgrad conv_3 128x320", 16, 64, 64, 128, 128, 320, 320),
+    ("L3 wgrad conv_3 256x640", 16, 32, 32, 256, 256, 640, 640),
+]
+
+
+def wsetup(lib, shp, dt):
+    name, N, Hh, Ww, aps, md, bps, nd = shp
+    code = H.dtype_code(dt)
+    P = N * Hh * Ww
+    a = torch.randn(P, aps, device="cuda").to(dt)
+    b = torch.randn(P, bps, device="cuda").to(dt)
+    wd = H.WgradDesc(dtype=code, gather=H.RDN_G_CONV3, n=N, h=Hh, w=Ww, hin=Hh, win=Ww, a=a.data_ptr(), a_ps=aps,
+                     a_c0=0, mdim=md, b=b.data_ptr(), b_ps=bps, b_c0=0, ndim=nd)
+    ns = lib.rdn_wgrad_splits(C.byref(wd))
+    wd.splits = ns
+    ws = torch.zeros(lib.rdn_wgrad_workspace_size(C.byref(wd)) // 4 + 64, device="cuda")
+    wd.ws = ws.data_ptr()
+    g = torch.zeros(md * nd * 9, device="cuda")
+    flops = 2.0 * P * md * 9 * nd
+    byts = 2 * P * (md + nd)
+    return wd, (a, b, ws, g), flops, byts, ns
+
+
+def wbench(L, libs, dt, st, reps):
+    only = os.environ.get("KB_ONLY", "")
+    for shp in WSHAPES:
+        if only and only not in shp[0]:
+            continue
+        setups = [wsetup(lib, shp, dt) for lib in L]
+        tw = [[] for _ in L]
+        tr = [[] for _ in L]
+        for rnd in range(3):
+            for i, lib in enumerate(L):
+                wd, (a, b, ws, g), _, _, ns = setups[i]
+                md, nd = shp[5], shp[7]
+                red = lambda: lib.rdn_wgrad_reduce(ws.data_ptr(), ns, md, nd, nd, 9, g.data_ptr(), 0, None, None, None, st)
+                for _ in range(2):
+                    lib.rdn_conv_wgrad(C.byref(wd), st)
+                    red()
+                e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+                e[0].record()
+                for _ in range(reps):
+                    rc = lib.rdn_conv_wgrad(C.byref(wd), st)
+                e[1].record()
+                for _ in range(reps):
+                    rc2 = red()
+                e[2].record()
+                torch.cuda.synchronize()
+                assert rc == 0 and rc2 == 0, lib.rdn_last_error()
+                tw[i].append(e[0].elapsed_time(e[1]) / reps)
+                tr[i].append(e[1].elapsed_time(e[2]) / reps)
+        res = []
+        for i in range(len(L)):
+            t, r = min(tw[i]), min(tr[i])
+            fl, by = setups[i][2], setups[i][3]
+            res.append(f"{t * 1e3:6.1f}+{r * 1e3:5.1f}us {fl / t / 1e9:4.0f}TF {by / t / 1e6:5.0f}GB s{setups[i][4]}")
+        print(f"{shp[0]:24s} " + " ".join(f"{x:>34s}" for x in res), flush=True)
+
+
 def main():
     libs = sys.argv[1:] or [H.LIB_PATH]
     L = [load(p) for p in libs]
@@ -79,7 +146,11 @@ def main():
     st = torch.cuda.current_stream().cuda_stream
     reps = int(os.environ.get("KB_REPS", "20"))
     print(f"{'shape':24s} " + " ".join(f"{os.path.basename(p)[:22]:>24s}" for p in libs))
+    if os.environ.get("KB_WGRAD", "1") != "0":
+        wbench(L, libs, dt, st, reps)
     only = os.environ.get("KB_ONLY", "")
+    if os.environ.get("KB_CONV", "1") == "0":
+        return
     for shp in SHAPES:
         if only and only not in shp[0]:
             continue

@@ -59,6 +59,8 @@ class PackItem(C.Structure):
 SIGNATURES = {
     "rdn_conv_fwd": (_i32, [C.POINTER(ConvDesc), _vp]),
     "rdn_conv_wgrad": (_i32, [C.POINTER(WgradDesc), _vp]),
+    "rdn_conv_kernel_name": (_i32, [C.POINTER(ConvDesc), C.c_char_p, _i32]),
+    "rdn_wgrad_kernel_name": (_i32, [C.POINTER(WgradDesc), C.c_char_p, _i32]),
     "rdn_wgrad_splits": (_i32, [C.POINTER(WgradDesc)]),
     "rdn_wgrad_chunks": (_i32, [C.POINTER(WgradDesc)]),
     "rdn_wgrad_workspace_size": (_i64, [C.POINTER(WgradDesc)]),

@@ -275,6 +275,7 @@ template <typename T, int BN, int WMW, int CK>
 int launch_h(const rdn_conv_desc* d, hipStream_t st) {
   const int tiles_x = (d->w + TW - 1) / TW, tiles_y = (d->h + TH - 1) / TH;
   dim3 grid((unsigned)(d->n * tiles_x * tiles_y), (unsigned)((d->ncols + BN - 1) / BN));
+  RDN_PROBE("conv3_halo_kernel<%s,%d,%d,%d%s>", rdn_tname<T>(), BN, WMW, CK, d->gate ? ",gate" : "");
   if (d->gate) {
     if constexpr (NT % (CK / TypeInfo<T>::VEC) == 0)
       conv3_halo_kernel<T, BN, WMW, CK, true><<<grid, NT, 0, st>>>(*d, tiles_x, tiles_y);

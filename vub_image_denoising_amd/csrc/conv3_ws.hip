@@ -81,7 +81,7 @@ __global__ __launch_bounds__(NT, 2) void conv3_ws_kernel(rdn_conv_desc d, int ti
   constexpr int E_IT = (EU + NT - 1) / NT;
   constexpr bool COLFIX = NT % UPR == 0;                 // a thread's output channels are tile-invariant
   constexpr bool KALIGN = CK % 32 == 0;                  // a k-step never straddles a tap
-  constexpr bool PF = E_IT <= 4;                         // epilogue operand prefetch (register budget)
+  constexpr bool PF = E_IT <= 6;                         // epilogue operand prefetch (register budget)
   static_assert(!GATE || NT % HU == 0, "fixed channel group per thread");
   static_assert(Cfg::FITS, "LDS");
 
@@ -159,7 +159,7 @@ __global__ __launch_bounds__(NT, 2) void conv3_ws_kernel(rdn_conv_desc d, int ti
   const int flags = d.flags;
   // fast epilogue: whole 16-B NHWC units, no NCHW output
   const bool fast_epi = (d.ncols % VEC) == 0 && !(flags & RDN_EPI_OUT_NCHW) &&
-                        (!(flags & RDN_EPI_RESID) || (d.res_climit >= d.ncols && d.res_ps % VEC == 0 &&
+                        (!(flags & RDN_EPI_RESID) || (d.res_climit % VEC == 0 && d.res_ps % VEC == 0 &&
                                                       d.res_c0 % VEC == 0)) &&
                         d.out_ps % VEC == 0 && d.out_c0 % VEC == 0 && d.pre_ps % VEC == 0;
   float ebias[COLFIX ? VEC : 1], ealpha[COLFIX ? VEC : 1];
@@ -244,7 +244,8 @@ __global__ __launch_bounds__(NT, 2) void conv3_ws_kernel(rdn_conv_desc d, int ti
 #pragma unroll
     for (int it = 0; it < E_IT; ++it) {
       if (it + 1 == E_IT && tid + it * NT >= EU) continue;
-      if (!COLFIX || col_of(it) < d.ncols) eop[it] = *(const u32x4*)(base + erel[it] * ps + col_of(it));
+      const int c = col_of(it);
+      if (c < (pf_res ? d.res_climit : d.ncols)) eop[it] = *(const u32x4*)(base + erel[it] * ps + c);
     }
   };
 
@@ -338,7 +339,7 @@ __global__ __launch_bounds__(NT, 2) void conv3_ws_kernel(rdn_conv_desc d, int ti
           bf16* const op = (bf16*)d.out + opix * d.out_ps + d.out_c0 + c;
           if (flags & (RDN_EPI_RESID | RDN_EPI_ACCUM)) {
             float rv[VEC];
-            if (flags & RDN_EPI_RESID) {
+            if ((flags & RDN_EPI_RESID) && c < d.res_climit) {
               Unit16<bf16>::unpack(pf_res ? eop[PF ? it : 0]
                                           : *(const u32x4*)((const bf16*)d.res + opix * d.res_ps + d.res_c0 + c),
                                    rv);
@@ -404,6 +405,7 @@ int launch_ws(const rdn_conv_desc* d, hipStream_t st) {
     if (slots < 1) slots = 1;
     dim3 grid((unsigned)(8 * slots));
     constexpr int HU = CK / 8;
+    if (!d->gate || NT % HU == 0) RDN_PROBE("conv3_ws_kernel<bf16,%d,%d%s>", BN, CK, d->gate ? ",gate" : "");
     if (d->gate) {
       if constexpr (NT % HU == 0)
         conv3_ws_kernel<BN, CK, true><<<grid, NT, 0, st>>>(*d, tiles_x, tiles_y, ntiles);

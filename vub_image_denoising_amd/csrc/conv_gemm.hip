@@ -230,6 +230,7 @@ int launch_gather(const rdn_conv_desc* d, hipStream_t st) {
   const int64_t M = (int64_t)d->n * d->h * d->w;
   dim3 grid((unsigned)((M + BM - 1) / BM), (unsigned)((d->ncols + BN - 1) / BN));
   FastDiv fw = make_fastdiv((uint32_t)d->w), fhw = make_fastdiv((uint32_t)(d->h * d->w));
+  RDN_PROBE("conv_gemm_kernel<%s,%d,%d,%d,%d>", rdn_tname<T>(), BM, BN, WMW, d->gather);
   switch (d->gather) {
     case RDN_G_CONV3: conv_gemm_kernel<T, BM, BN, WMW, RDN_G_CONV3><<<grid, NT, 0, st>>>(*d, fw, fhw); break;
     case RDN_G_S2: conv_gemm_kernel<T, BM, BN, WMW, RDN_G_S2><<<grid, NT, 0, st>>>(*d, fw, fhw); break;

@@ -269,6 +269,7 @@ static int launch_g(const rdn_wgrad_desc* d, hipStream_t st) {
   pchunk = (pchunk + KP - 1) / KP * KP;
   dim3 grid((d->mdim + BM - 1) / BM, (taps * d->ndim + BN - 1) / BN, splits);
   FastDiv fw = make_fastdiv((uint32_t)d->w), fhw = make_fastdiv((uint32_t)(d->h * d->w));
+  RDN_PROBE("wgrad_kernel<%s,%d,%d,%d,%d>", rdn_tname<T>(), BM, BN, WMW, d->gather);
   if (d->gather == RDN_G_CONV3)
     wgrad_kernel<T, BM, BN, WMW, RDN_G_CONV3><<<grid, NT, 0, st>>>(*d, fw, fhw, (int)pchunk);
   else

@@ -24,6 +24,34 @@ int rdn_check_launch(const char* what) {
   return RDN_OK;
 }
 extern "C" const char* rdn_last_error(void) { return g_err; }
+
+thread_local char* rdn_probe_buf = nullptr;
+thread_local int rdn_probe_len = 0;
+int rdn_probe_name(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(rdn_probe_buf, (size_t)rdn_probe_len, fmt, ap);
+  va_end(ap);
+  return RDN_OK;
+}
+extern "C" int rdn_conv_kernel_name(const rdn_conv_desc* d, char* buf, int32_t len) {
+  if (!buf || len < 1) { rdn_set_error("rdn_conv_kernel_name: no buffer"); return RDN_E_ARG; }
+  buf[0] = 0;
+  rdn_probe_buf = buf;
+  rdn_probe_len = len;
+  const int rc = rdn_conv_fwd(d, nullptr);
+  rdn_probe_buf = nullptr;
+  return rc;
+}
+extern "C" int rdn_wgrad_kernel_name(const rdn_wgrad_desc* d, char* buf, int32_t len) {
+  if (!buf || len < 1) { rdn_set_error("rdn_wgrad_kernel_name: no buffer"); return RDN_E_ARG; }
+  buf[0] = 0;
+  rdn_probe_buf = buf;
+  rdn_probe_len = len;
+  const int rc = rdn_conv_wgrad(d, nullptr);
+  rdn_probe_buf = nullptr;
+  return rc;
+}
 extern "C" const char* rdn_version(void) { return "rdunet_hip 0.1.0 gfx950"; }
 
 namespace {

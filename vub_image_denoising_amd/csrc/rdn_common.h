@@ -90,3 +90,15 @@ int rdn_wgrad3_chunks(const rdn_wgrad_desc* d);
 // error plumbing (host)
 void rdn_set_error(const char* fmt, ...);
 int rdn_check_launch(const char* what);
+
+// launch probe (rdn_conv_kernel_name / rdn_wgrad_kernel_name): while set, the
+// launchers write the name of the kernel instantiation they would launch and
+// return without launching
+extern thread_local char* rdn_probe_buf;
+extern thread_local int rdn_probe_len;
+int rdn_probe_name(const char* fmt, ...);
+#define RDN_PROBE(...) \
+  do {                 \
+    if (rdn_probe_buf) return rdn_probe_name(__VA_ARGS__); \
+  } while (0)
+template <typename T> constexpr const char* rdn_tname() { return sizeof(T) == 2 ? "bf16" : "f32"; }

@@ -277,7 +277,247 @@ __global__ __launch_bounds__(NT, 2) void wgrad3_halo_kernel(rdn_wgrad_desc d, in
   }
 }
 
-struct Plan { int bm, ck, mtiles, chunks, tiles_x, tiles_y, ntiles, tpb, splits; };
+// bf16 variant with wide channel groups (CK up to 96: whole level-0 pixel rows,
+// so dY and X are each read once per launch in full rows) and no per-tile
+// index math in the k loop: every LDS operand address is a per-thread base
+// fixed for the launch plus an immediate, and the tile loaders add one
+// precomputed per-unit offset to a per-tile base.
+template <int BM, int CK, bool GATE>
+__global__ __launch_bounds__(NT, 2) void wgrad3_rows_kernel(rdn_wgrad_desc d, int tiles_x, int tiles_y, int ntiles,
+                                                            int tiles_per_block) {
+  constexpr int VEC = 8;
+  constexpr int NCOL = 9 * CK;
+  constexpr int NT_ALL = (NCOL + 15) / 16;
+  constexpr int NTW = (NT_ALL + 3) / 4;     // n-tiles per wave (n-tile = wave + 4 j)
+  constexpr int MT = BM / 16;
+  constexpr int DROW = tr_stride(BM * 2);
+  constexpr int HROW = tr_stride(CK * 2);
+  constexpr int DU = BM / VEC, HU = CK / VEC;   // 16-B units per pixel row
+  constexpr int D_UNITS = TP * DU, H_UNITS = HP * HU;
+  constexpr int D_IT = (D_UNITS + NT - 1) / NT, H_IT = (H_UNITS + NT - 1) / NT;
+  constexpr int D_BYTES = TP * DROW;
+  constexpr int MAIN_BYTES = D_BYTES + HP * HROW;
+  constexpr int RED_BYTES = GATE ? 2 * NT * VEC * 4 : 0;
+  static_assert(NT % DU == 0, "fixed dY channel group per thread");
+  __shared__ __attribute__((aligned(16))) unsigned char lds[MAIN_BYTES > RED_BYTES ? MAIN_BYTES : RED_BYTES];
+  unsigned char* const dyl = lds;
+  unsigned char* const hal = lds + D_BYTES;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, g = lane >> 4;
+  const int m0 = blockIdx.x * BM;
+  const int c0 = blockIdx.y * CK;
+  const int t_beg = blockIdx.z * tiles_per_block;
+  const int t_end = min(t_beg + tiles_per_block, ntiles);
+  const int H = d.h, W = d.w;
+  const bf16* __restrict__ A = (const bf16*)d.a;
+  const bf16* __restrict__ Bx = (const bf16*)d.b;
+  const bf16* __restrict__ G = (const bf16*)d.a_gate;
+
+  // ---- per-thread unit geometry (tile-invariant)
+  const int acg = tid % DU;                     // this thread's dY channel group
+  const bool m_ok = m0 + acg * VEC < d.mdim;
+  int drel[D_IT], grel[GATE ? D_IT : 1], dlds[D_IT], dpix[D_IT];
+#pragma unroll
+  for (int it = 0; it < D_IT; ++it) {
+    const int u = tid + it * NT;
+    const int p = u / DU;
+    dpix[it] = p;
+    drel[it] = ((p / TW) * W + p % TW) * (int)d.a_ps + d.a_c0 + m0 + acg * VEC;
+    if constexpr (GATE) grel[it] = ((p / TW) * W + p % TW) * (int)d.a_gate_ps + m0 + acg * VEC;
+    dlds[it] = p * DROW + acg * 16;
+  }
+  constexpr bool HLIN = HROW == HU * 16;        // unpadded halo rows: LDS offset = unit * 16
+  int hrel[H_IT], hlds[HLIN ? 1 : H_IT];
+#pragma unroll
+  for (int it = 0; it < H_IT; ++it) {
+    const int u = tid + it * NT;
+    const int hp = u / HU, cu = u - hp * HU;
+    const int hy = hp / (TW + 2), hx = hp - hy * (TW + 2);
+    hrel[it] = (hy * W + hx) * (int)d.b_ps + d.b_c0 + c0 + cu * VEC;
+    if constexpr (!HLIN) hlds[it] = hp * HROW + cu * 16;
+  }
+
+  float galpha[GATE ? VEC : 1], sa[GATE ? VEC : 1], sb[GATE ? VEC : 1];
+  const bool do_part = GATE && d.part != nullptr && blockIdx.y == 0;
+  if constexpr (GATE) {
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) {
+      const int m = m0 + acg * VEC + q;
+      galpha[q] = m < d.mdim ? d.a_gate_alpha[m] : 0.f;
+      sa[q] = 0.f;
+      sb[q] = 0.f;
+    }
+  }
+
+  u32x4 dreg[D_IT], greg[GATE ? D_IT : 1], hreg[H_IT];
+  auto load_tile = [&](int t) {
+    const int tx = t % tiles_x, r1 = t / tiles_x;
+    const int ty = r1 % tiles_y, nimg = r1 / tiles_y;
+    const int y0 = ty * TH, x0 = tx * TW;
+    const int64_t pix0 = ((int64_t)nimg * H + y0) * W + x0;
+    const bool full = y0 + TH <= H && x0 + TW <= W;
+    const bf16* const ab = A + pix0 * d.a_ps;
+    const bf16* const gb = GATE ? G + pix0 * d.a_gate_ps : nullptr;
+#pragma unroll
+    for (int it = 0; it < D_IT; ++it) {
+      const int p = dpix[it];
+      bool ok = m_ok && ((it + 1 < D_IT) || tid + it * NT < D_UNITS);
+      if (!full) ok = ok && y0 + p / TW < H && x0 + p % TW < W;
+      u32x4 v = {0u, 0u, 0u, 0u}, gv = {0u, 0u, 0u, 0u};
+      if (ok) {
+        v = *(const u32x4*)(ab + drel[it]);
+        if constexpr (GATE) gv = *(const u32x4*)(gb + grel[it]);
+      }
+      dreg[it] = v;
+      if constexpr (GATE) greg[it] = gv;
+    }
+    const bf16* const hb = Bx + (pix0 - W - 1) * d.b_ps;   // halo pixel (0, 0) = image (y0 - 1, x0 - 1)
+    const bool interior = y0 >= 1 && y0 + TH + 1 <= H && x0 >= 1 && x0 + TW + 1 <= W;
+#pragma unroll
+    for (int it = 0; it < H_IT; ++it) {
+      const int u = tid + it * NT;
+      bool ok = (it + 1 < H_IT) || u < H_UNITS;
+      if (!interior) {
+        const int hp = u / HU;
+        const int hy = hp / (TW + 2), hx = hp - hy * (TW + 2);
+        ok = ok && (unsigned)(y0 - 1 + hy) < (unsigned)H && (unsigned)(x0 - 1 + hx) < (unsigned)W;
+      }
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (ok) v = *(const u32x4*)(hb + hrel[it]);
+      hreg[it] = v;
+    }
+  };
+  auto store_tile = [&]() {
+#pragma unroll
+    for (int it = 0; it < D_IT; ++it) {
+      if (it + 1 == D_IT && tid + it * NT >= D_UNITS) continue;
+      u32x4 v = dreg[it];
+      if constexpr (GATE) {
+        float dy[VEC], pr[VEC];
+        Unit16<bf16>::unpack(v, dy);
+        Unit16<bf16>::unpack(greg[it], pr);
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) {
+          const bool pos = pr[q] > 0.f;
+          if (!pos) sa[q] += pr[q] * dy[q];
+          dy[q] = pos ? dy[q] : galpha[q] * dy[q];
+        }
+        v = Unit16<bf16>::pack(dy);
+        if (do_part) {  // dbias sums dYpre before its rounding, as rdn_prelu_bwd does
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) sb[q] += dy[q];
+        }
+      }
+      *(u32x4*)(dyl + dlds[it]) = v;
+    }
+#pragma unroll
+    for (int it = 0; it < H_IT; ++it) {
+      if (it + 1 == H_IT && tid + it * NT >= H_UNITS) continue;
+      *(u32x4*)(hal + (HLIN ? (tid + it * NT) * 16 : hlds[HLIN ? 0 : it])) = hreg[it];
+    }
+  };
+
+  f32x4 acc[MT][NTW];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // lane (g, q = li>>2, pp = li&3) supplies pixels {4g+q, 16+4g+q} of each 32-pixel
+  // k-step and columns 4pp..4pp+3 of each 16-wide tile (ds_read_b64_tr_b16)
+  const int q = li >> 2, pp = li & 3;
+  const unsigned char* const pa = dyl + (4 * g + q) * DROW + 4 * pp * 2;
+  const unsigned char* const pb = hal + (4 * g + q) * HROW;
+  int boff[NTW];
+#pragma unroll
+  for (int j = 0; j < NTW; ++j) {
+    const int c = (wave + 4 * j) * 16 + 4 * pp;
+    const int cc = c < NCOL ? c : 0;          // padded columns: valid reads, never stored
+    const int tp = cc / CK, ci = cc - (cc / CK) * CK;
+    boff[j] = ((tp / 3) * (TW + 2) + tp % 3) * HROW + ci * 2;
+  }
+
+  if (t_beg < t_end) {
+    load_tile(t_beg);
+    store_tile();
+  }
+  __syncthreads();
+  for (int t = t_beg; t < t_end; ++t) {
+    if (t + 1 < t_end) load_tile(t + 1);
+#pragma unroll
+    for (int ks = 0; ks < TP / 32; ++ks) {
+      bf16x8 af[MT];
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, pa + (ks * 32) * DROW + i * 32));
+        const i16x4 hi =
+            __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, pa + (ks * 32 + 16) * DROW + i * 32));
+        af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) {
+        if (wave + 4 * j >= NT_ALL) continue;
+        const unsigned char* b = pb + boff[j] + ks * 2 * (TW + 2) * HROW;
+        const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, b));
+        const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, b + (TW + 2) * HROW));
+        const bf16x8 bfr = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+        for (int i = 0; i < MT; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][j], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+    if (t + 1 < t_end) {
+      store_tile();
+      __syncthreads();
+    }
+  }
+
+  if constexpr (GATE) {
+    if (do_part) {
+      float* red = (float*)lds;  // the tile loop ended with a barrier
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) {
+        red[tid * VEC + k] = sa[k];
+        red[NT * VEC + tid * VEC + k] = sb[k];
+      }
+      __syncthreads();
+      if (tid < BM) {
+        const int cg = tid / VEC, k = tid % VEC;
+        float a = 0.f, b = 0.f;
+        for (int r = 0; r < NT / DU; ++r) {
+          a += red[(r * DU + cg) * VEC + k];
+          b += red[NT * VEC + (r * DU + cg) * VEC + k];
+        }
+        const int m = m0 + tid;
+        if (m < d.mdim) {
+          d.part[((int64_t)blockIdx.z * 2 + 0) * d.mdim + m] = a;
+          d.part[((int64_t)blockIdx.z * 2 + 1) * d.mdim + m] = b;
+        }
+      }
+    }
+  }
+  // D[m][n]: row = g*4 + e (output channel), col = li (tile column)
+  const int ncol_all = 9 * d.ndim;
+  float* __restrict__ ws = d.ws + (int64_t)blockIdx.z * d.mdim * ncol_all;
+#pragma unroll
+  for (int j = 0; j < NTW; ++j) {
+    const int nt = wave + 4 * j;
+    const int c = nt * 16 + li;
+    if (nt >= NT_ALL || c >= NCOL) continue;
+    const int tp = c / CK, ci = c - tp * CK;
+    const int col = tp * d.ndim + c0 + ci;
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = m0 + i * 16 + g * 4 + e;
+        if (m < d.mdim) ws[(int64_t)m * ncol_all + col] = acc[i][j][e];
+      }
+  }
+}
+
+struct Plan { int bm, ck, rows, mtiles, chunks, tiles_x, tiles_y, ntiles, tpb, splits; };
 
 Plan plan(const rdn_wgrad_desc* d) {
   Plan p;
@@ -286,8 +526,17 @@ Plan plan(const rdn_wgrad_desc* d) {
   const int cap = d->dtype == RDN_BF16 ? (p.bm <= 32 ? 64 : 32) : 32;
   while (ck > cap) ck >>= 1;
   p.ck = ck;
+  p.rows = 0;
+#ifndef RDN_NO_WROWS
+  if (d->dtype == RDN_BF16) {
+    // rows kernel: the widest channel group whose accumulators fit (BM x 9 CK per block)
+    static const int cands[] = {96, 80, 64, 48, 32, 16, 8};
+    for (int c : cands)
+      if (d->ndim % c == 0 && c * p.bm <= 2560) { p.ck = c; p.rows = 1; break; }
+  }
+#endif
   p.mtiles = (d->mdim + p.bm - 1) / p.bm;
-  p.chunks = d->ndim / ck;
+  p.chunks = d->ndim / p.ck;
   p.tiles_x = (d->w + TW - 1) / TW;
   p.tiles_y = (d->h + TH - 1) / TH;
   p.ntiles = d->n * p.tiles_x * p.tiles_y;
@@ -304,11 +553,43 @@ Plan plan(const rdn_wgrad_desc* d) {
 template <typename T, int BM, int CK>
 int launch_w(const rdn_wgrad_desc* d, const Plan& p, hipStream_t st) {
   dim3 grid(p.mtiles, p.chunks, p.splits);
+  RDN_PROBE("wgrad3_halo_kernel<%s,%d,%d%s>", rdn_tname<T>(), BM, CK, d->a_gate ? ",gate" : "");
   if (d->a_gate)
     wgrad3_halo_kernel<T, BM, CK, true><<<grid, NT, 0, st>>>(*d, p.tiles_x, p.tiles_y, p.ntiles, p.tpb);
   else
     wgrad3_halo_kernel<T, BM, CK, false><<<grid, NT, 0, st>>>(*d, p.tiles_x, p.tiles_y, p.ntiles, p.tpb);
   return rdn_check_launch("rdn_conv_wgrad(conv3)");
+}
+
+template <int BM, int CK>
+int launch_rows(const rdn_wgrad_desc* d, const Plan& p, hipStream_t st) {
+  if constexpr (CK * BM > 2560) {
+    rdn_set_error("rdn_conv_wgrad(conv3): rows kernel BM=%d CK=%d", BM, CK);
+    return RDN_E_SHAPE;
+  } else {
+    dim3 grid(p.mtiles, p.chunks, p.splits);
+    RDN_PROBE("wgrad3_rows_kernel<bf16,%d,%d%s>", BM, CK, d->a_gate ? ",gate" : "");
+    if (d->a_gate)
+      wgrad3_rows_kernel<BM, CK, true><<<grid, NT, 0, st>>>(*d, p.tiles_x, p.tiles_y, p.ntiles, p.tpb);
+    else
+      wgrad3_rows_kernel<BM, CK, false><<<grid, NT, 0, st>>>(*d, p.tiles_x, p.tiles_y, p.ntiles, p.tpb);
+    return rdn_check_launch("rdn_conv_wgrad(conv3 rows)");
+  }
+}
+
+template <int BM>
+int launch_rows_ck(const rdn_wgrad_desc* d, const Plan& p, hipStream_t st) {
+  switch (p.ck) {
+    case 96: return launch_rows<BM, 96>(d, p, st);
+    case 80: return launch_rows<BM, 80>(d, p, st);
+    case 64: return launch_rows<BM, 64>(d, p, st);
+    case 48: return launch_rows<BM, 48>(d, p, st);
+    case 32: return launch_rows<BM, 32>(d, p, st);
+    case 16: return launch_rows<BM, 16>(d, p, st);
+    case 8: return launch_rows<BM, 8>(d, p, st);
+  }
+  rdn_set_error("rdn_conv_wgrad(conv3): bad chunk %d", p.ck);
+  return RDN_E_SHAPE;
 }
 
 template <typename T, int BM>
@@ -331,6 +612,11 @@ int rdn_wgrad3_chunks(const rdn_wgrad_desc* d) { return plan(d).chunks; }
 int rdn_wgrad3_launch(const rdn_wgrad_desc* d, hipStream_t st) {
   const Plan p = plan(d);
   if (p.ck <= 0) { rdn_set_error("rdn_conv_wgrad(conv3): ndim=%d", d->ndim); return RDN_E_SHAPE; }
+  if (p.rows) {
+    if (p.bm == 16) return launch_rows_ck<16>(d, p, st);
+    if (p.bm == 32) return launch_rows_ck<32>(d, p, st);
+    return launch_rows_ck<64>(d, p, st);
+  }
   if (d->dtype == RDN_BF16) {
     if (p.bm == 16) return launch_ck<bf16, 16>(d, p, st);
     if (p.bm == 32) return launch_ck<bf16, 32>(d, p, st);

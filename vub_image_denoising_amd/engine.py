@@ -537,32 +537,30 @@ class UNetEngine:
             if L.extra["fused"]:
                 L.wgrad_desc.part = self.pws.data_ptr()
 
+    @staticmethod
+    def _probe_copy(desc, cls, keep):
+        """Copy of a descriptor whose per-call pointers (bound at launch time) are
+        stand-ins, for the dispatch probe; pointers that select a kernel variant
+        (`keep`) stay as they are."""
+        d = cls.from_buffer_copy(desc)
+        for name, typ in cls._fields_:
+            if name not in keep and issubclass(typ, (C.c_void_p, C._Pointer)) and not getattr(d, name):
+                setattr(d, name, C.cast(C.c_void_p(4096), typ) if typ is not C.c_void_p else 4096)
+        return d
+
     def _kernel_key(self, desc):
-        """Name of the kernel template instantiation a conv descriptor launches
-        (matches the rocprofv3 kernel name, demangled)."""
-        dt = "bf16" if self.code == H.RDN_BF16 else "f32"
-        bn = 16 if desc.ncols <= 16 else 32 if desc.ncols <= 32 else 64 if desc.ncols <= 64 else 128
-        wmw = 4 if bn <= 32 else 2
-        if desc.gather == H.RDN_G_CONV3:
-            ck = H.lib().rdn_conv3_chunk(desc.cin, self.code)
-            bn = H.lib().rdn_conv3_pick_bn(desc.ncols)
-            wmw = 2 if bn in (64, 128) else 4
-            return f"conv3_halo_kernel<{dt},{bn},{wmw},{ck}>"
-        return f"conv_gemm_kernel<{dt},128,{bn},{wmw},{desc.gather}>"
+        """Name of the kernel instantiation a conv descriptor launches, as the
+        library's own dispatch decides it (rdn_conv_kernel_name)."""
+        d = self._probe_copy(desc, H.ConvDesc, ("gate", "gate_alpha"))
+        buf = C.create_string_buffer(128)
+        H.check(H.lib().rdn_conv_kernel_name(C.byref(d), buf, 128), "rdn_conv_kernel_name")
+        return buf.value.decode()
 
     def _wgrad_key(self, wg):
-        dt = "bf16" if self.code == H.RDN_BF16 else "f32"
-        if wg.gather == H.RDN_G_CONV3:
-            bm = 16 if wg.mdim <= 16 else 32 if wg.mdim <= 32 else 64
-            cap = (64 if bm <= 32 else 32) if self.code == H.RDN_BF16 else 32
-            ck = cap
-            while ck > 8 and wg.ndim % ck:
-                ck //= 2
-            return f"wgrad3_halo_kernel<{dt},{bm},{ck}>"
-        bm = 16 if wg.mdim <= 16 else 32 if wg.mdim <= 32 else 64
-        bn = 64 if 4 * wg.ndim <= 64 else 128
-        wmw = 1 if bm == 16 else 2
-        return f"wgrad_kernel<{dt},{bm},{bn},{wmw},{wg.gather}>"
+        d = self._probe_copy(wg, H.WgradDesc, ("a_gate", "a_gate_alpha", "part"))
+        buf = C.create_string_buffer(128)
+        H.check(H.lib().rdn_wgrad_kernel_name(C.byref(d), buf, 128), "rdn_wgrad_kernel_name")
+        return buf.value.decode()
 
     def _build_info(self):
         """Per launch: kernel instantiation key + algorithmic FLOPs and bytes
