@@ -93,7 +93,7 @@ def wsetup(lib, shp, dt):
     b = torch.randn(P, bps, device="cuda").to(dt)
     wd = H.WgradDesc(dtype=code, gather=H.RDN_G_CONV3, n=N, h=Hh, w=Ww, hin=Hh, win=Ww, a=a.data_ptr(), a_ps=aps,
                      a_c0=0, mdim=md, b=b.data_ptr(), b_ps=bps, b_c0=0, ndim=nd)
-    ns = lib.rdn_wgrad_splits(C.byref(wd))
+    ns = int(os.environ.get("KB_SPLITS", "0")) or lib.rdn_wgrad_splits(C.byref(wd))
     wd.splits = ns
     ws = torch.zeros(lib.rdn_wgrad_workspace_size(C.byref(wd)) // 4 + 64, device="cuda")
     wd.ws = ws.data_ptr()

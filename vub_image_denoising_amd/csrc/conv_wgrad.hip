@@ -208,32 +208,41 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
     }
     return;
   }
-  const int cpb = 256 / sl_count;
-  const int cc = threadIdx.x % cpb, sl = threadIdx.x / cpb;
+  // 4 consecutive columns per thread (16-B loads), sl_count split lanes per
+  // column quad, lanes combined in LDS in a fixed order (deterministic)
+  const int qpb = 256 / sl_count;                 // column quads per block
+  const int cq = threadIdx.x % qpb, sl = threadIdx.x / qpb;
   const int ncol = taps * ndim;
-  const int64_t total = (int64_t)mdim * ncol;
-  const int64_t o = (int64_t)blockIdx.x * cpb + cc;
-  float s = 0.f;
+  const int64_t total = (int64_t)mdim * ncol;     // multiple of 4 (ndim % 8 == 0)
+  const int64_t o = ((int64_t)blockIdx.x * qpb + cq) * 4;
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
   if (o < total) {
+    const float* p = ws + o;
     int z = sl;
     for (; z + 3 * sl_count < splits; z += 4 * sl_count) {
-      const float a0 = ws[(int64_t)z * total + o], a1 = ws[(int64_t)(z + sl_count) * total + o];
-      const float a2 = ws[(int64_t)(z + 2 * sl_count) * total + o], a3 = ws[(int64_t)(z + 3 * sl_count) * total + o];
+      const f32x4 a0 = *(const f32x4*)(p + (int64_t)z * total);
+      const f32x4 a1 = *(const f32x4*)(p + (int64_t)(z + sl_count) * total);
+      const f32x4 a2 = *(const f32x4*)(p + (int64_t)(z + 2 * sl_count) * total);
+      const f32x4 a3 = *(const f32x4*)(p + (int64_t)(z + 3 * sl_count) * total);
       s += (a0 + a1) + (a2 + a3);
     }
-    for (; z < splits; z += sl_count) s += ws[(int64_t)z * total + o];
+    for (; z < splits; z += sl_count) s += *(const f32x4*)(p + (int64_t)z * total);
   }
-  __shared__ float red[256];
+  __shared__ f32x4 red[256];
   red[threadIdx.x] = s;
   __syncthreads();
   if (sl == 0 && o < total) {
-    for (int q = 1; q < sl_count; ++q) s += red[q * cpb + cc];
+    for (int q = 1; q < sl_count; ++q) s += red[q * qpb + cq];
     const int m = (int)(o / ncol);
-    const int col = (int)(o - (int64_t)m * ncol);
-    const int tap = col / ndim, nd = col - tap * ndim;
-    if (nd < ndim_real) {
-      const int64_t dst = ((int64_t)m * ndim_real + nd) * taps + tap;
-      grad[dst] = accumulate ? grad[dst] + s : s;
+    const int col0 = (int)(o - (int64_t)m * ncol);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int col = col0 + e;
+      const int tap = col / ndim, nd = col - tap * ndim;
+      if (nd < ndim_real) {
+        const int64_t dst = ((int64_t)m * ndim_real + nd) * taps + tap;
+        grad[dst] = accumulate ? grad[dst] + s[e] : s[e];
+      }
     }
   }
 }
@@ -331,10 +340,11 @@ extern "C" int rdn_wgrad_reduce(const float* ws, int32_t splits, int32_t mdim, i
     rdn_set_error("rdn_wgrad_reduce: bad arguments"); return RDN_E_ARG;
   }
   const int64_t total = (int64_t)mdim * ndim * taps;
+  if (ndim % 4 || ((uintptr_t)ws & 15)) { rdn_set_error("rdn_wgrad_reduce: ndim %% 4 / alignment"); return RDN_E_ARG; }
   int sl = 1;
   while (sl < 16 && sl < splits) sl <<= 1;
-  const int cpb = 256 / sl;
-  int64_t blocks = (total + cpb - 1) / cpb;
+  const int qpb = 256 / sl;
+  int64_t blocks = (total / 4 + qpb - 1) / qpb;
   if (part && blocks < 2 * mdim) blocks = 2 * mdim;
   if (blocks > 0x7fffffff) { rdn_set_error("rdn_wgrad_reduce: too large"); return RDN_E_SHAPE; }
   dim3 grid((unsigned)blocks, part ? 2 : 1);
