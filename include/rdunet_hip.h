@@ -122,10 +122,11 @@ int64_t rdn_wgrad_workspace_size(const rdn_wgrad_desc* d);
 /* grad[(m*ndim_real+nd)*taps+tap] (+)= sum_s ws[s][m][tap*ndim+nd] for nd < ndim_real:
    the reference's OIHW (Conv2d) / IOHW (ConvTranspose2d) order.  With `part`
    non-NULL also dalpha[m] += sum_s part[s][0][m], dbias[m] += sum_s part[s][1][m]
-   (fixed summation order: deterministic). */
+   over s < part_splits (0: = splits) -- the partials of a gated rdn_conv_wgrad or
+   of rdn_prelu_bwd run without dalpha/dbias (fixed summation order: deterministic). */
 int rdn_wgrad_reduce(const float* ws, int32_t splits, int32_t mdim, int32_t ndim, int32_t ndim_real,
                      int32_t taps, float* grad, int32_t accumulate,
-                     const float* part, float* dalpha, float* dbias, void* stream);
+                     const float* part, int32_t part_splits, float* dalpha, float* dbias, void* stream);
 
 /* PReLU backward (+ conv bias gradient) over a pixel grid of `pixels` pixels:
    dyp[p, c] = dy[p, c] * (pre[p, c] > 0 ? 1 : alpha[c])   (c < C; 0 for C <= c < cpad)
@@ -137,6 +138,9 @@ int rdn_prelu_bwd(int32_t dtype, int64_t pixels, int32_t n, int32_t h, int32_t w
                   void* dyp, float* dalpha, float* dbias, float* ws, void* stream);
 /* per-block channel partials (deterministic, no atomics): bytes of `ws` needed */
 int64_t rdn_prelu_bwd_workspace_size(int32_t dtype, int64_t pixels, int32_t C, int32_t cpad);
+/* number of [2][C] partial rows rdn_prelu_bwd leaves in ws; with dalpha and dbias
+   both NULL it stops there and rdn_wgrad_reduce (part_splits = this) sums them */
+int32_t rdn_prelu_bwd_blocks(int32_t dtype, int64_t pixels, int32_t cpad);
 
 /* x[b] = a_b*noisy[b] + (1-a_b)*clean[b], a_b = tnorm[b]; fp32 NCHW, `per` elements per image */
 int rdn_interp(const float* clean, const float* noisy, const float* tnorm, int32_t batch, int64_t per,

@@ -18,8 +18,9 @@ from vub_image_denoising_amd import _hip as H  # noqa: E402
 def load(path):
     lib = C.CDLL(path)
     for name, (res, args) in H.SIGNATURES.items():
-        fn = getattr(lib, name)
-        fn.restype, fn.argtypes = res, args
+        fn = getattr(lib, name, None)   # older variant builds may lack newer entry points
+        if fn is not None:
+            fn.restype, fn.argtypes = res, args
     return lib
 
 
@@ -115,7 +116,7 @@ def wbench(L, libs, dt, st, reps):
             for i, lib in enumerate(L):
                 wd, (a, b, ws, g), _, _, ns = setups[i]
                 md, nd = shp[5], shp[7]
-                red = lambda: lib.rdn_wgrad_reduce(ws.data_ptr(), ns, md, nd, nd, 9, g.data_ptr(), 0, None, None, None, st)
+                red = lambda: lib.rdn_wgrad_reduce(ws.data_ptr(), ns, md, nd, nd, 9, g.data_ptr(), 0, None, 0, None, None, st)
                 for _ in range(2):
                     lib.rdn_conv_wgrad(C.byref(wd), st)
                     red()

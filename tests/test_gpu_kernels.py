@@ -171,7 +171,7 @@ def _wgrad(dt, gather, N, h, w, hin, win, A, a_ps, a_c0, mdim, B, b_ps, b_c0, nd
     d.ws = ws.data_ptr()
     H.check(lib.rdn_conv_wgrad(C.byref(d), H.stream_ptr()))
     g = torch.zeros(mdim * ndim_real * taps, device="cuda")
-    H.check(lib.rdn_wgrad_reduce(ws.data_ptr(), ns, mdim, ndim, ndim_real, taps, g.data_ptr(), 0, None, None, None,
+    H.check(lib.rdn_wgrad_reduce(ws.data_ptr(), ns, mdim, ndim, ndim_real, taps, g.data_ptr(), 0, None, 0, None, None,
                                  H.stream_ptr()))
     torch.cuda.synchronize()
     return g
@@ -380,7 +380,7 @@ def test_fused_prelu_gate_matches_separate_pass(dt):
         g = torch.zeros(cout * cin * 9, device="cuda")
         H.check(lib.rdn_conv_wgrad(C.byref(wd), st))
         H.check(lib.rdn_wgrad_reduce(ws.data_ptr(), ns, cout, cin, cin, 9, g.data_ptr(), 0,
-                                     part.data_ptr() if gate else None, da.data_ptr() if gate else None,
+                                     part.data_ptr() if gate else None, 0, da.data_ptr() if gate else None,
                                      db.data_ptr() if gate else None, st))
         return g
 
@@ -393,6 +393,26 @@ def test_fused_prelu_gate_matches_separate_pass(dt):
     assert torch.equal(o1, o2)
     assert torch.equal(g1, g2)
     assert _rel(da2, da1) < 1e-5 and _rel(db2, db1) < 1e-5
+    # unfused path as the engine runs it: rdn_prelu_bwd leaves its partials, the
+    # layer's rdn_wgrad_reduce sums them (part_splits = rdn_prelu_bwd_blocks)
+    pws2 = torch.zeros_like(pws)
+    H.check(lib.rdn_prelu_bwd(code, P, N, Hh, Ww, cout, cout, dyb.data_ptr(), Cd, 48, None, pre.data_ptr(), cout,
+                              a.data_ptr(), dyp.data_ptr(), None, None, pws2.data_ptr(), st))
+    nb = lib.rdn_prelu_bwd_blocks(code, P, cout)
+    da3, db3 = torch.zeros(cout, device="cuda"), torch.zeros(cout, device="cuda")
+    wd = H.WgradDesc(dtype=code, gather=H.RDN_G_CONV3, n=N, h=Hh, w=Ww, hin=Hh, win=Ww, a=dyp.data_ptr(), a_ps=cout,
+                     a_c0=0, mdim=cout, b=x.data_ptr(), b_ps=Cs, b_c0=0, ndim=cin)
+    ns = lib.rdn_wgrad_splits(C.byref(wd))
+    wd.splits = ns
+    ws = torch.zeros(lib.rdn_wgrad_workspace_size(C.byref(wd)) // 4, device="cuda")
+    wd.ws = ws.data_ptr()
+    g3 = torch.zeros(cout * cin * 9, device="cuda")
+    H.check(lib.rdn_conv_wgrad(C.byref(wd), st))
+    H.check(lib.rdn_wgrad_reduce(ws.data_ptr(), ns, cout, cin, cin, 9, g3.data_ptr(), 0, pws2.data_ptr(), nb,
+                                 da3.data_ptr(), db3.data_ptr(), st))
+    torch.cuda.synchronize()
+    assert torch.equal(g3, g1)
+    assert _rel(da3, da1) < 1e-5 and _rel(db3, db1) < 1e-5
 
 
 @pytest.mark.parametrize("cin,cout,Cs_in,gate,accum", [

@@ -64,7 +64,8 @@ SIGNATURES = {
     "rdn_wgrad_splits": (_i32, [C.POINTER(WgradDesc)]),
     "rdn_wgrad_chunks": (_i32, [C.POINTER(WgradDesc)]),
     "rdn_wgrad_workspace_size": (_i64, [C.POINTER(WgradDesc)]),
-    "rdn_wgrad_reduce": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _vp, _i32, _vp, _vp, _vp, _vp]),
+    "rdn_wgrad_reduce": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _vp, _i32, _vp, _i32, _vp, _vp, _vp]),
+    "rdn_prelu_bwd_blocks": (_i32, [_i32, _i64, _i32]),
     "rdn_prelu_bwd": (_i32, [_i32, _i64, _i32, _i32, _i32, _i32, _i32, _vp, _i64, _i32, _vp, _vp, _i64, _vp,
                              _vp, _vp, _vp, _vp, _vp]),
     "rdn_prelu_bwd_workspace_size": (_i64, [_i32, _i64, _i32, _i32]),

@@ -17,7 +17,7 @@
 // steps of 8 units (128 B per row), double buffered with a register prefetch
 // of the next stage.  bf16: v_mfma_f32_16x16x32_bf16, fp32: v_mfma_f32_16x16x4_f32
 // (exact fp32, the mode parity is checked in).
-#include "rdn_common.h"
+#include "conv3_tile.h"
 
 namespace {
 
@@ -172,56 +172,53 @@ __global__ __launch_bounds__(NT) void conv_gemm_kernel(rdn_conv_desc d, FastDiv 
 
 #undef ldsA
 #undef ldsB
-  // ---- fused epilogue
-  const int flags = d.flags;
-  T* __restrict__ OUT = (T*)d.out;
-  T* __restrict__ PRE = (T*)d.pre;
-  const T* __restrict__ RES = (const T*)d.res;
-  const int H = d.h, W = d.w;
+  // ---- fused epilogue: the fp32 tile goes through LDS (the K loop ended with a
+  // barrier) so every global access is a 16-byte unit of VEC channels of one
+  // output pixel; with SCATTER2 the unit's columns are VEC channels of one tap
+  // (cout % VEC == 0), i.e. one 16-B piece of a depth-to-space output pixel.
+  static_assert(BM * (BN + 4) * 4 <= 2 * (BM + BN) * ROWB, "epilogue tile fits the K-loop LDS");
+  constexpr int CROW = BN + 4;
+  float* const Ct = (float*)lds;
 #pragma unroll
-  for (int j = 0; j < NTL; ++j) {
-    const int col = n0 + wn * WTN + j * 16 + (lane & 15);
-    if (col >= d.ncols) continue;
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NTL; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        Ct[(wm * WTM + i * 16 + (lane >> 4) * 4 + e) * CROW + wn * WTN + j * 16 + (lane & 15)] = acc[i][j][e];
+  __syncthreads();
+  const int flags = d.flags;
+  const int H = d.h, W = d.w;
+  constexpr int UPR = BN / VEC;
+#pragma nounroll
+  for (int u = tid; u < BM * UPR; u += NT) {
+    const int r = u / UPR, cu = u - r * UPR;
+    const int64_t m = m0 + r;
+    const int col = n0 + cu * VEC;
+    if (m >= M || col >= d.ncols) continue;
     int c = col, tp = 0;
     if (flags & RDN_EPI_SCATTER2) { tp = col / d.cout; c = col - tp * d.cout; }
-    const float bias = (flags & RDN_EPI_BIAS) ? d.bias[c] : 0.f;
-    const float alpha = (flags & RDN_EPI_PRELU) ? d.alpha[c] : 0.f;
-#pragma unroll
-    for (int i = 0; i < MT; ++i) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int64_t m = m0 + wm * WTM + i * 16 + (lane >> 4) * 4 + e;
-        if (m >= M) continue;
-        float v = acc[i][j][e] + bias;
-        int64_t opix = m;
-        int nimg = 0, y = 0, x = 0, Ho = H, Wo = W;
-        if (flags & (RDN_EPI_SCATTER2 | RDN_EPI_OUT_NCHW)) {
-          nimg = (int)fdiv((uint32_t)m, fd_hw);
-          const int rem = (int)m - nimg * H * W;
-          y = (int)fdiv((uint32_t)rem, fd_w);
-          x = rem - y * W;
-          if (flags & RDN_EPI_SCATTER2) {
-            Ho = 2 * H; Wo = 2 * W;
-            y = 2 * y + (tp >> 1);
-            x = 2 * x + (tp & 1);
-            opix = ((int64_t)nimg * Ho + y) * Wo + x;
-          }
-        }
-        if (flags & RDN_EPI_STORE_PRE) PRE[opix * d.pre_ps + c] = from_f32<T>(v);
-        if (flags & RDN_EPI_PRELU) v = v > 0.f ? v : alpha * v;
-        if (flags & RDN_EPI_OUT_NCHW) {
-          const int64_t o = (((int64_t)nimg * d.cout + c) * Ho + y) * Wo + x;
-          if (flags & RDN_EPI_RESID) v += d.res_nchw[o];
-          if (flags & RDN_EPI_ACCUM) v += d.out_nchw[o];
-          d.out_nchw[o] = v;
-        } else {
-          if ((flags & RDN_EPI_RESID) && c < d.res_climit) v += to_f32(RES[opix * d.res_ps + d.res_c0 + c]);
-          T* op = OUT + opix * d.out_ps + d.out_c0 + c;
-          if (flags & RDN_EPI_ACCUM) v += to_f32(*op);
-          *op = from_f32<T>(v);
-        }
+    int64_t opix = m;
+    int nimg = 0, y = 0, x = 0;
+    if (flags & (RDN_EPI_SCATTER2 | RDN_EPI_OUT_NCHW)) {
+      nimg = (int)fdiv((uint32_t)m, fd_hw);
+      const int rem = (int)m - nimg * H * W;
+      y = (int)fdiv((uint32_t)rem, fd_w);
+      x = rem - y * W;
+      if (flags & RDN_EPI_SCATTER2) {
+        y = 2 * y + (tp >> 1);
+        x = 2 * x + (tp & 1);
+        opix = ((int64_t)nimg * (2 * H) + y) * (2 * W) + x;
       }
     }
+    float v[VEC];
+    const float* src = Ct + r * CROW + cu * VEC;
+#pragma unroll
+    for (int q = 0; q < VEC; q += 4) {
+      const f32x4 t4 = *(const f32x4*)(src + q);
+      v[q] = t4[0]; v[q + 1] = t4[1]; v[q + 2] = t4[2]; v[q + 3] = t4[3];
+    }
+    c3::finish_unit<T>(d, v, c, opix, y, x, nimg, c3::PF_NONE, u32x4{0u, 0u, 0u, 0u});
   }
 }
 
@@ -274,7 +271,10 @@ extern "C" int rdn_conv_fwd(const rdn_conv_desc* d, void* stream) {
   if (d->gather == RDN_G_S2 && (d->hin != 2 * d->h || d->win != 2 * d->w)) { rdn_set_error("rdn_conv_fwd: s2 grid mismatch"); return RDN_E_SHAPE; }
   if (d->gather != RDN_G_S2 && (d->hin != d->h || d->win != d->w)) { rdn_set_error("rdn_conv_fwd: grid mismatch"); return RDN_E_SHAPE; }
   if ((int64_t)d->n * d->h * d->w >= (1ll << 31)) { rdn_set_error("rdn_conv_fwd: too many pixels"); return RDN_E_SHAPE; }
-  if ((d->flags & RDN_EPI_SCATTER2) && (d->cout * 4 != d->ncols)) { rdn_set_error("rdn_conv_fwd: scatter needs ncols=4*cout"); return RDN_E_SHAPE; }
+  if ((d->flags & RDN_EPI_SCATTER2) && (d->cout * 4 != d->ncols || d->cout % vec || (d->flags & RDN_EPI_OUT_NCHW))) {
+    rdn_set_error("rdn_conv_fwd: scatter needs ncols=4*cout, cout %% %d == 0, NHWC output", vec);
+    return RDN_E_SHAPE;
+  }
   if ((d->flags & RDN_EPI_OUT_NCHW) ? !d->out_nchw : !d->out) { rdn_set_error("rdn_conv_fwd: null output"); return RDN_E_ARG; }
   if ((d->flags & RDN_EPI_BIAS) && !d->bias) { rdn_set_error("rdn_conv_fwd: null bias"); return RDN_E_ARG; }
   if ((d->flags & RDN_EPI_PRELU) && !d->alpha) { rdn_set_error("rdn_conv_fwd: null alpha"); return RDN_E_ARG; }

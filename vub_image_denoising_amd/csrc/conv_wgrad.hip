@@ -189,12 +189,13 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(rdn_wgrad_desc d, FastDiv fd_
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int mdim, int ndim,
                                                            int ndim_real, int taps, float* __restrict__ grad,
                                                            int accumulate, int sl_count, const float* __restrict__ part,
-                                                           float* __restrict__ dalpha, float* __restrict__ dbias) {
+                                                           int part_splits, float* __restrict__ dalpha,
+                                                           float* __restrict__ dbias) {
   if (blockIdx.y == 1) {  // fused-PReLU partials: one block per (channel, dalpha|dbias), fixed order
     if (blockIdx.x >= 2 * mdim) return;
     const int which = blockIdx.x / mdim, m = blockIdx.x - which * mdim;
     float s = 0.f;
-    for (int z = threadIdx.x; z < splits; z += 256) s += part[((int64_t)z * 2 + which) * mdim + m];
+    for (int z = threadIdx.x; z < part_splits; z += 256) s += part[((int64_t)z * 2 + which) * mdim + m];
     __shared__ float red1[256];
     red1[threadIdx.x] = s;
     __syncthreads();
@@ -334,8 +335,8 @@ extern "C" int rdn_conv_wgrad(const rdn_wgrad_desc* d, void* stream) {
 }
 
 extern "C" int rdn_wgrad_reduce(const float* ws, int32_t splits, int32_t mdim, int32_t ndim, int32_t ndim_real,
-                                int32_t taps, float* grad, int32_t accumulate, const float* part, float* dalpha,
-                                float* dbias, void* stream) {
+                                int32_t taps, float* grad, int32_t accumulate, const float* part, int32_t part_splits,
+                                float* dalpha, float* dbias, void* stream) {
   if (!ws || !grad || splits <= 0 || mdim <= 0 || ndim <= 0 || ndim_real <= 0 || ndim_real > ndim || taps <= 0) {
     rdn_set_error("rdn_wgrad_reduce: bad arguments"); return RDN_E_ARG;
   }
@@ -349,6 +350,7 @@ extern "C" int rdn_wgrad_reduce(const float* ws, int32_t splits, int32_t mdim, i
   if (blocks > 0x7fffffff) { rdn_set_error("rdn_wgrad_reduce: too large"); return RDN_E_SHAPE; }
   dim3 grid((unsigned)blocks, part ? 2 : 1);
   wgrad_reduce_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(ws, splits, mdim, ndim, ndim_real, taps, grad, accumulate,
-                                                            sl, part, dalpha, dbias);
+                                                            sl, part, part_splits > 0 ? part_splits : splits, dalpha,
+                                                            dbias);
   return rdn_check_launch("rdn_wgrad_reduce");
 }

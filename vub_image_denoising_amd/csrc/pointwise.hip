@@ -414,6 +414,10 @@ static int prelu_blocks(int dtype, int64_t pixels, int cpad) {
   return grid_for(pixels, ppb * 8, 1024);
 }
 
+extern "C" int32_t rdn_prelu_bwd_blocks(int32_t dtype, int64_t pixels, int32_t cpad) {
+  return prelu_blocks(dtype, pixels, cpad);
+}
+
 extern "C" int64_t rdn_prelu_bwd_workspace_size(int32_t dtype, int64_t pixels, int32_t C, int32_t cpad) {
   return (int64_t)prelu_blocks(dtype, pixels, cpad) * 2 * C * (int64_t)sizeof(float);
 }

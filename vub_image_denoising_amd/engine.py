@@ -633,17 +633,19 @@ class UNetEngine:
             pre = self.bufs[L.pre]
             ga, gb = L.extra["grad_a"], L.extra["grad_b"]
             fused = L.extra["fused"]
+            # unfused: the PReLU-backward pass leaves its dalpha/dbias partials in
+            # pws for this layer's rdn_wgrad_reduce to sum (no finalize launch)
             if fused:
                 rc = 0
             elif L.ddst is None:
                 rc = lib.rdn_prelu_bwd(self.code, P, n, h, w, L.cout, L.cout_pad, None, 0, 0, dy.data_ptr(),
                                        pre.data_ptr(), pre.shape[1], self.named[L.act + ".weight"].data_ptr(),
-                                       dyp, ga.data_ptr(), gb.data_ptr(), self.pws.data_ptr(), st)
+                                       dyp, None, None, self.pws.data_ptr(), st)
             else:
                 dd = self.bufs[L.ddst.buf]
                 rc = lib.rdn_prelu_bwd(self.code, P, n, h, w, L.cout, L.cout_pad, dd.data_ptr(), dd.shape[1],
                                        L.ddst.c0, None, pre.data_ptr(), pre.shape[1],
-                                       self.named[L.act + ".weight"].data_ptr(), dyp, ga.data_ptr(), gb.data_ptr(),
+                                       self.named[L.act + ".weight"].data_ptr(), dyp, None, None,
                                        self.pws.data_ptr(), st)
             if rc:
                 H.check(rc, f"prelu_bwd[{L.name}]")
@@ -661,13 +663,10 @@ class UNetEngine:
             if rc:
                 H.check(rc, f"wgrad[{L.name}]")
             splits, mdim, ndim, ndim_real, taps = L.extra["wgrad"]
-            if fused:
-                rc = lib.rdn_wgrad_reduce(self.ws.data_ptr(), splits, mdim, ndim, ndim_real, taps,
-                                          L.extra["grad_w"].data_ptr(), 1, self.pws.data_ptr(), ga.data_ptr(),
-                                          gb.data_ptr(), st)
-            else:
-                rc = lib.rdn_wgrad_reduce(self.ws.data_ptr(), splits, mdim, ndim, ndim_real, taps,
-                                          L.extra["grad_w"].data_ptr(), 1, None, None, None, st)
+            part_splits = 0 if fused else lib.rdn_prelu_bwd_blocks(self.code, P, L.cout_pad)
+            rc = lib.rdn_wgrad_reduce(self.ws.data_ptr(), splits, mdim, ndim, ndim_real, taps,
+                                      L.extra["grad_w"].data_ptr(), 1, self.pws.data_ptr(), part_splits,
+                                      ga.data_ptr(), gb.data_ptr(), st)
             if rc:
                 H.check(rc, f"wgrad_reduce[{L.name}]")
             if sync is not None:
