@@ -35,6 +35,7 @@ __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_
   constexpr int ES = sizeof(T);
   constexpr int VEC = TypeInfo<T>::VEC;
   constexpr int SK = 128 / ES;                       // k per stage
+  constexpr int KSTEP = 4 * VEC;                     // k per MFMA step (4 lane groups x one 16-B unit)
   constexpr int CKB = CK * ES;                       // bytes per halo pixel row (data)
   constexpr int HROW = HaloRow<CKB>::V;
   constexpr int SPC = (9 * CK + SK - 1) / SK;        // stages per chunk
@@ -52,11 +53,15 @@ __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_
   constexpr int CROW = BN * 4 + 16;                  // epilogue fp32 tile row
   constexpr int EPI_BYTES = BM * CROW;
   constexpr int LDS_BYTES = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
+  constexpr bool KALIGN = CK % KSTEP == 0;           // a k-step never straddles a tap
+  constexpr int UPR = BN / VEC, EU = BM * UPR, E_IT = (EU + NT - 1) / NT;
+  constexpr bool COLFIX = NT % UPR == 0;             // a thread's output channels are fixed
   static_assert(MT >= 1 && NTL >= 1 && (CK % VEC) == 0, "tile");
+  static_assert(!GATE || NT % HU == 0, "fixed channel group per thread");
 
   __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
   unsigned char* const halo = lds;
-#define ldsB(b) (lds + HALO_BYTES + (b) * (BN * ROWB))
+  unsigned char* const bst = lds + HALO_BYTES;      // two weight stages of BN x ROWB
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WMW, wn = wave / WMW;
@@ -67,39 +72,40 @@ __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_
   const int nimg = bt / tiles_y;
   const int y0 = ty * TH, x0 = tx * TW;
   const int n0 = blockIdx.y * BN;
-  const T* __restrict__ X = (const T*)d.x;
-  const T* __restrict__ WP = (const T*)d.wp;
   const int H = d.h, W = d.w;
   const int nch = d.cin / CK;
-  const int nst = nch * SPC;
 
-  // ---- halo loader: unit u -> (halo pixel, 16-B channel group).  With GATE
-  // the unit is dY and becomes dYpre = dY * (pre > 0 ? 1 : alpha) when it is
-  // written to LDS (PReLU backward fused into the input-gradient conv).
-  static_assert(!GATE || NT % HU == 0, "fixed channel group per thread");
+  // ---- halo units of this thread (tile fixed for the block): element offset
+  // from the halo origin, LDS offset, in-image flag; chunk c adds c * CK
+  const int64_t hpix0 = ((int64_t)nimg * H + (y0 - 1)) * W + (x0 - 1);
+  const T* const xb = (const T*)d.x + hpix0 * d.x_ps + d.x_c0;
+  const T* const gb = GATE ? (const T*)d.gate + hpix0 * d.gate_ps : nullptr;
+  int hrel[H_IT], grel[GATE ? H_IT : 1], hlds[H_IT];
+  bool hok[H_IT];
+#pragma unroll
+  for (int it = 0; it < H_IT; ++it) {
+    const int u = tid + it * NT;
+    const int hp = u / HU, cu = u - hp * HU;
+    const int hy = hp / (TW + 2), hx = hp - hy * (TW + 2);
+    hok[it] = u < H_UNITS && (unsigned)(y0 - 1 + hy) < (unsigned)H && (unsigned)(x0 - 1 + hx) < (unsigned)W;
+    hrel[it] = (hy * W + hx) * (int)d.x_ps + cu * VEC;
+    if constexpr (GATE) grel[it] = (hy * W + hx) * (int)d.gate_ps + cu * VEC;
+    hlds[it] = u < H_UNITS ? hp * HROW + cu * 16 : -1;
+  }
   u32x4 hreg[H_IT];
   u32x4 greg[GATE ? H_IT : 1];
   float galpha[GATE ? VEC : 1];
-  const T* __restrict__ G = (const T*)d.gate;
   auto load_halo = [&](int c) {
     if constexpr (GATE) {
-      const int ch = c * CK + (tid % HU) * VEC;
 #pragma unroll
-      for (int q = 0; q < VEC; ++q) galpha[q] = d.gate_alpha[ch + q];
+      for (int q = 0; q < VEC; ++q) galpha[q] = d.gate_alpha[c * CK + (tid % HU) * VEC + q];
     }
 #pragma unroll
     for (int it = 0; it < H_IT; ++it) {
-      const int u = tid + it * NT;
       u32x4 v = {0u, 0u, 0u, 0u}, gv = {0u, 0u, 0u, 0u};
-      if (u < H_UNITS) {
-        const int hp = u / HU, cu = u - hp * HU;
-        const int hy = hp / (TW + 2), hx = hp - hy * (TW + 2);
-        const int yy = y0 + hy - 1, xx = x0 + hx - 1;
-        if (yy >= 0 && yy < H && xx >= 0 && xx < W) {
-          const int64_t pix = ((int64_t)nimg * H + yy) * W + xx;
-          v = *(const u32x4*)(X + pix * d.x_ps + d.x_c0 + c * CK + cu * VEC);
-          if constexpr (GATE) gv = *(const u32x4*)(G + pix * d.gate_ps + c * CK + cu * VEC);
-        }
+      if (hok[it]) {
+        v = *(const u32x4*)(xb + hrel[it] + c * CK);
+        if constexpr (GATE) gv = *(const u32x4*)(gb + grel[it] + c * CK);
       }
       hreg[it] = v;
       if constexpr (GATE) greg[it] = gv;
@@ -108,41 +114,49 @@ __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_
   auto store_halo = [&]() {
 #pragma unroll
     for (int it = 0; it < H_IT; ++it) {
-      const int u = tid + it * NT;
-      if (u < H_UNITS) {
-        const int hp = u / HU, cu = u - hp * HU;
-        u32x4 v = hreg[it];
-        if constexpr (GATE) {
-          float dy[VEC], pr[VEC];
-          Unit16<T>::unpack(v, dy);
-          Unit16<T>::unpack(greg[it], pr);
+      if (hlds[it] < 0) continue;
+      u32x4 v = hreg[it];
+      if constexpr (GATE) {
+        float dy[VEC], pr[VEC];
+        Unit16<T>::unpack(v, dy);
+        Unit16<T>::unpack(greg[it], pr);
 #pragma unroll
-          for (int q = 0; q < VEC; ++q) dy[q] = pr[q] > 0.f ? dy[q] : galpha[q] * dy[q];
-          v = Unit16<T>::pack(dy);
-        }
-        *(u32x4*)(halo + hp * HROW + cu * 16) = v;
+        for (int q = 0; q < VEC; ++q) dy[q] = pr[q] > 0.f ? dy[q] : galpha[q] * dy[q];
+        v = Unit16<T>::pack(dy);
       }
+      *(u32x4*)(halo + hlds[it]) = v;
     }
   };
-  // ---- weight stage loader: 8 units (128 B) per output channel
+  // ---- weight stages: 8 units (128 B) per output channel; stage (c, j) at c*KC + j*SK
   u32x4 breg[B_IT];
   const int ku = tid & 7;
-  auto load_b = [&](int s) {
-    const int c = s / SPC, j = s - c * SPC;
+  const T* const wb = (const T*)d.wp + (int64_t)(n0 + (tid >> 3)) * d.kp + ku * VEC;
+  auto load_b = [&](int c, int j) {
 #pragma unroll
-    for (int it = 0; it < B_IT; ++it) {
-      const int u = tid + it * NT;
-      if (u < B_UNITS)
-        breg[it] = *(const u32x4*)(WP + (int64_t)(n0 + (u >> 3)) * d.kp + (int64_t)c * KC + j * SK + ku * VEC);
-    }
+    for (int it = 0; it < B_IT; ++it)
+      if (tid + it * NT < B_UNITS) breg[it] = *(const u32x4*)(wb + (int64_t)it * (NT / 8) * d.kp + c * KC + j * SK);
   };
   auto store_b = [&](int buf) {
 #pragma unroll
-    for (int it = 0; it < B_IT; ++it) {
-      const int u = tid + it * NT;
-      if (u < B_UNITS) *(u32x4*)(ldsB(buf) + (u >> 3) * ROWB + ku * 16) = breg[it];
-    }
+    for (int it = 0; it < B_IT; ++it)
+      if (tid + it * NT < B_UNITS) *(u32x4*)(bst + buf * (BN * ROWB) + ((tid >> 3) + it * (NT / 8)) * ROWB + ku * 16) = breg[it];
   };
+
+  // ---- fragment addresses: per-lane base + immediates
+  const int a_lane = ((wm * (WTM / 16)) * (TW + 2) + r) * HROW;
+  int offA[KALIGN ? 1 : 2 * SPC];
+  if constexpr (!KALIGN) {
+#pragma unroll
+    for (int jk = 0; jk < 2 * SPC; ++jk) {
+      const int k = jk * KSTEP + g * VEC;
+      int tap = k / CK;
+      const int ci = k - tap * CK;
+      tap = tap < 9 ? tap : 8;   // padded k: zero weights, finite operand
+      offA[jk] = a_lane + ((tap / 3) * (TW + 2) + tap % 3) * HROW + ci * ES;
+    }
+  }
+  const unsigned char* const pa = halo + (KALIGN ? a_lane + g * 16 : 0);
+  const int b_lane = (wn * WTN + r) * ROWB + g * 16;
 
   f32x4 acc[MT][NTL];
 #pragma unroll
@@ -150,27 +164,24 @@ __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_
 #pragma unroll
     for (int jn = 0; jn < NTL; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // tile-local pixel of m-tile i, lane row r: (py, px) = (wm*WTM/16 + i, r)
-  const int py0 = wm * (WTM / 16);
-
-  auto compute = [&](int s) {
-    const int c = s / SPC, j = s - c * SPC;
-    const int buf = s & 1;
+  auto compute = [&](int j, const unsigned char* pbs) {   // stage j of the current chunk
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      // this lane group's first k within the chunk
-      const int k = j * SK + ks * (4 * VEC) + g * VEC;
-      int tap = k / CK;
-      const int ci = k - tap * CK;
-      tap = tap < 9 ? tap : 8;  // padded k: zero weights, finite operand
-      const int ky = tap / 3, kx = tap - 3 * ky;
+      int ao;
+      if constexpr (KALIGN) {
+        const int k0 = (2 * j + ks) * KSTEP;
+        int tap = k0 / CK;
+        const int ci = k0 - tap * CK;
+        tap = tap < 9 ? tap : 8;
+        ao = ((tap / 3) * (TW + 2) + tap % 3) * HROW + ci * ES;
+      } else {
+        ao = offA[2 * j + ks];
+      }
       u32x4 af[MT], bfr[NTL];
 #pragma unroll
-      for (int i = 0; i < MT; ++i)
-        af[i] = *(const u32x4*)(halo + ((py0 + i + ky) * (TW + 2) + (r + kx)) * HROW + ci * ES);
+      for (int i = 0; i < MT; ++i) af[i] = *(const u32x4*)(pa + ao + i * (TW + 2) * HROW);
 #pragma unroll
-      for (int jn = 0; jn < NTL; ++jn)
-        bfr[jn] = *(const u32x4*)(ldsB(buf) + (wn * WTN + jn * 16 + r) * ROWB + ks * 64 + g * 16);
+      for (int jn = 0; jn < NTL; ++jn) bfr[jn] = *(const u32x4*)(pbs + jn * 16 * ROWB + ks * 64);
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -190,74 +201,30 @@ __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_
   };
 
   load_halo(0);
+  load_b(0, 0);
   store_halo();
-#if defined(RDN_HALO_PF2)
-  // weights prefetched TWO stages ahead in two register sets (even / odd stage)
-  u32x4 breg2[B_IT];
-  auto load_b2 = [&](int s, u32x4* R) {
-    const int c = s / SPC, j = s - c * SPC;
-#pragma unroll
-    for (int it = 0; it < B_IT; ++it) {
-      const int u = tid + it * NT;
-      if (u < B_UNITS)
-        R[it] = *(const u32x4*)(WP + (int64_t)(n0 + (u >> 3)) * d.kp + (int64_t)c * KC + j * SK + ku * VEC);
-    }
-  };
-  auto store_b2 = [&](int buf, const u32x4* R) {
-#pragma unroll
-    for (int it = 0; it < B_IT; ++it) {
-      const int u = tid + it * NT;
-      if (u < B_UNITS) *(u32x4*)(ldsB(buf) + (u >> 3) * ROWB + ku * 16) = R[it];
-    }
-  };
-  load_b2(0, breg);
-  store_b2(0, breg);
-  if (nst > 1) load_b2(1, breg2);
-  __syncthreads();
-  auto step = [&](int s, u32x4* Rfree, const u32x4* Rnext) {
-    const int c = s / SPC, j = s - c * SPC;
-    if (j == 0 && c + 1 < nch) load_halo(c + 1);
-    if (s + 2 < nst) load_b2(s + 2, Rfree);
-    compute(s);
-    if (s + 1 < nst) store_b2((s + 1) & 1, Rnext);
-    __syncthreads();
-    if (j == SPC - 1 && c + 1 < nch) {
-      store_halo();
-      __syncthreads();
-    }
-  };
-  int s = 0;
-  for (; s + 1 < nst; s += 2) {
-    step(s, breg, breg2);
-    step(s + 1, breg2, breg);
-  }
-  if (s < nst) step(s, breg, breg2);
-#else
-  load_b(0);
   store_b(0);
   __syncthreads();
-
-  for (int s = 0; s < nst; ++s) {
-    const int c = s / SPC, j = s - c * SPC;
-    const bool last_of_chunk = (j == SPC - 1);
-    if (j == 0 && c + 1 < nch) load_halo(c + 1);
-#if !defined(RDN_HALO_NOLOADB)
-    if (s + 1 < nst) load_b(s + 1);
-#endif
-    compute(s);
-#if !defined(RDN_HALO_NOLOADB)
-    if (s + 1 < nst) store_b((s & 1) ^ 1);
-#endif
-    __syncthreads();
-    if (last_of_chunk && c + 1 < nch) {
+  int buf = 0;
+  for (int c = 0; c < nch; ++c) {
+    const bool more = c + 1 < nch;
+    if (more) load_halo(c + 1);   // in flight during this chunk's SPC stages
+#pragma unroll
+    for (int j = 0; j < SPC; ++j) {
+      const bool nxt = j + 1 < SPC || more;
+      if (nxt) load_b(j + 1 < SPC ? c : c + 1, j + 1 < SPC ? j + 1 : 0);
+      compute(j, bst + buf * (BN * ROWB) + b_lane);
+      if (nxt) store_b(buf ^ 1);
+      __syncthreads();
+      buf ^= 1;
+    }
+    if (more) {
       store_halo();
       __syncthreads();
     }
   }
-#endif
-#undef ldsB
 
-  // ---- epilogue: fp32 tile through LDS, then 16-byte NHWC stores
+  // ---- epilogue: fp32 tile through LDS, then 16-byte NHWC units
   float* const Ct = (float*)lds;
 #pragma unroll
   for (int i = 0; i < MT; ++i)
@@ -268,7 +235,65 @@ __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_
         Ct[((wm * WTM + i * 16 + g * 4 + e) * CROW) / 4 + wn * WTN + jn * 16 + r] = acc[i][jn][e];
   __syncthreads();
 
-  c3::store_tile<T, BN, NT>(d, Ct, CROW / 4, y0, x0, nimg, n0, tid);
+  const int flags = d.flags;
+  const bool fast = (d.ncols % VEC) == 0 && !(flags & RDN_EPI_OUT_NCHW) && y0 + TH <= H && x0 + TW <= W &&
+                    (!(flags & RDN_EPI_RESID) || (d.res_climit % VEC == 0 && d.res_ps % VEC == 0 &&
+                                                  d.res_c0 % VEC == 0)) &&
+                    d.out_ps % VEC == 0 && d.out_c0 % VEC == 0 && d.pre_ps % VEC == 0;
+  if (!fast) {
+    c3::store_tile<T, BN, NT>(d, Ct, CROW / 4, y0, x0, nimg, n0, tid);
+    return;
+  }
+  const int64_t opix0 = ((int64_t)nimg * H + y0) * W + x0;
+  float ebias[VEC], ealpha[VEC];
+  if constexpr (COLFIX) {
+    const int c = n0 + (tid % UPR) * VEC;
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) {
+      ebias[q] = ((flags & RDN_EPI_BIAS) && c + q < d.ncols) ? d.bias[c + q] : 0.f;
+      ealpha[q] = ((flags & RDN_EPI_PRELU) && c + q < d.ncols) ? d.alpha[c + q] : 0.f;
+    }
+  }
+#pragma unroll
+  for (int it = 0; it < E_IT; ++it) {
+    const int u = tid + it * NT;
+    if (it + 1 == E_IT && u >= EU) continue;
+    const int px = u / UPR, cl = (u - px * UPR) * VEC, c = n0 + cl;
+    if (c >= d.ncols) continue;
+    float v[VEC];
+    const float* src = Ct + (px * CROW) / 4 + cl;
+#pragma unroll
+    for (int q = 0; q < VEC; q += 4) {
+      const f32x4 t4 = *(const f32x4*)(src + q);
+      v[q] = t4[0]; v[q + 1] = t4[1]; v[q + 2] = t4[2]; v[q + 3] = t4[3];
+    }
+    const int64_t opix = opix0 + (px / TW) * W + px % TW;
+    if (flags & RDN_EPI_BIAS) {
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) v[q] += COLFIX ? ebias[q] : d.bias[c + q];
+    }
+    if (flags & RDN_EPI_STORE_PRE) *(u32x4*)((T*)d.pre + opix * d.pre_ps + c) = Unit16<T>::pack(v);
+    if (flags & RDN_EPI_PRELU) {
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) {
+        const float a = COLFIX ? ealpha[q] : d.alpha[c + q];
+        v[q] = v[q] > 0.f ? v[q] : a * v[q];
+      }
+    }
+    T* const op = (T*)d.out + opix * d.out_ps + d.out_c0 + c;
+    float rv[VEC];
+    if ((flags & RDN_EPI_RESID) && c < d.res_climit) {
+      Unit16<T>::unpack(*(const u32x4*)((const T*)d.res + opix * d.res_ps + d.res_c0 + c), rv);
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) v[q] += rv[q];
+    }
+    if (flags & RDN_EPI_ACCUM) {
+      Unit16<T>::unpack(*(const u32x4*)op, rv);
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) v[q] += rv[q];
+    }
+    *(u32x4*)op = Unit16<T>::pack(v);
+  }
 }
 
 template <typename T, int BN, int WMW, int CK>
