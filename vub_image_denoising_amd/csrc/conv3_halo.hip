@@ -66,12 +66,16 @@ __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WMW, wn = wave / WMW;
   const int r = lane & 15, g = lane >> 4;
-  int bt = blockIdx.x;
+  // 1-D grid, logical (column tile, pixel tile) with the column tile fastest: the
+  // blocks reading one input halo share an XCD (xcd_remap)
+  const int ncb = (d.ncols + BN - 1) / BN;
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  int bt = lb / ncb;
   const int tx = bt % tiles_x; bt /= tiles_x;
   const int ty = bt % tiles_y;
   const int nimg = bt / tiles_y;
   const int y0 = ty * TH, x0 = tx * TW;
-  const int n0 = blockIdx.y * BN;
+  const int n0 = (lb - (lb / ncb) * ncb) * BN;
   const int H = d.h, W = d.w;
   const int nch = d.cin / CK;
 
@@ -299,7 +303,7 @@ __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_
 template <typename T, int BN, int WMW, int CK>
 int launch_h(const rdn_conv_desc* d, hipStream_t st) {
   const int tiles_x = (d->w + TW - 1) / TW, tiles_y = (d->h + TH - 1) / TH;
-  dim3 grid((unsigned)(d->n * tiles_x * tiles_y), (unsigned)((d->ncols + BN - 1) / BN));
+  dim3 grid((unsigned)(d->n * tiles_x * tiles_y * ((d->ncols + BN - 1) / BN)));
   RDN_PROBE("conv3_halo_kernel<%s,%d,%d,%d%s>", rdn_tname<T>(), BN, WMW, CK, d->gate ? ",gate" : "");
   if (d->gate) {
     if constexpr (NT % (CK / TypeInfo<T>::VEC) == 0)

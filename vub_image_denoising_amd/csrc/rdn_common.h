@@ -61,6 +61,15 @@ template <> struct Unit16<bf16> {
   }
 };
 
+// XCD-aware block order (MI355X: workgroups are dispatched round-robin over the 8
+// XCDs, each with its own L2): logical ids [k*nb/8, (k+1)*nb/8) all run on XCD k,
+// so consecutive logical blocks -- which the kernels make share input tiles --
+// meet in one L2.  Bijective for any nb (cdna_hip_programming.md T1).
+__device__ __forceinline__ int xcd_remap(int b, int nb) {
+  const int xcd = b & 7, q = nb >> 3, r = nb & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
+
 // Fast unsigned division by a runtime-invariant divisor (n < 2^31).
 struct FastDiv {
   uint32_t d, m, s;

@@ -305,9 +305,16 @@ __global__ __launch_bounds__(NT, 2) void wgrad3_rows_kernel(rdn_wgrad_desc d, in
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, g = lane >> 4;
-  const int m0 = blockIdx.x * BM;
-  const int c0 = blockIdx.y * CK;
-  const int t_beg = blockIdx.z * tiles_per_block;
+  // 1-D grid, logical (m-tile, chunk, split) with the m-tile fastest.  With one
+  // block per split, consecutive splits (adjacent pixel ranges: shared halo rows)
+  // go to one XCD (xcd_remap); with several blocks per split the plain order
+  // measured faster (scripts/kbench.py, L1-L3 shapes)
+  const int mtiles = (d.mdim + BM - 1) / BM, nchunks = d.ndim / CK;
+  const int lb = mtiles * nchunks == 1 ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int bx = lb % mtiles, by = (lb / mtiles) % nchunks, bz = lb / (mtiles * nchunks);
+  const int m0 = bx * BM;
+  const int c0 = by * CK;
+  const int t_beg = bz * tiles_per_block;
   const int t_end = min(t_beg + tiles_per_block, ntiles);
   const int H = d.h, W = d.w;
   const bf16* __restrict__ A = (const bf16*)d.a;
@@ -339,7 +346,7 @@ __global__ __launch_bounds__(NT, 2) void wgrad3_rows_kernel(rdn_wgrad_desc d, in
   }
 
   float galpha[GATE ? VEC : 1], sa[GATE ? VEC : 1], sb[GATE ? VEC : 1];
-  const bool do_part = GATE && d.part != nullptr && blockIdx.y == 0;
+  const bool do_part = GATE && d.part != nullptr && by == 0;
   if constexpr (GATE) {
 #pragma unroll
     for (int q = 0; q < VEC; ++q) {
@@ -491,15 +498,15 @@ __global__ __launch_bounds__(NT, 2) void wgrad3_rows_kernel(rdn_wgrad_desc d, in
         }
         const int m = m0 + tid;
         if (m < d.mdim) {
-          d.part[((int64_t)blockIdx.z * 2 + 0) * d.mdim + m] = a;
-          d.part[((int64_t)blockIdx.z * 2 + 1) * d.mdim + m] = b;
+          d.part[((int64_t)bz * 2 + 0) * d.mdim + m] = a;
+          d.part[((int64_t)bz * 2 + 1) * d.mdim + m] = b;
         }
       }
     }
   }
   // D[m][n]: row = g*4 + e (output channel), col = li (tile column)
   const int ncol_all = 9 * d.ndim;
-  float* __restrict__ ws = d.ws + (int64_t)blockIdx.z * d.mdim * ncol_all;
+  float* __restrict__ ws = d.ws + (int64_t)bz * d.mdim * ncol_all;
 #pragma unroll
   for (int j = 0; j < NTW; ++j) {
     const int nt = wave + 4 * j;
@@ -567,7 +574,7 @@ int launch_rows(const rdn_wgrad_desc* d, const Plan& p, hipStream_t st) {
     rdn_set_error("rdn_conv_wgrad(conv3): rows kernel BM=%d CK=%d", BM, CK);
     return RDN_E_SHAPE;
   } else {
-    dim3 grid(p.mtiles, p.chunks, p.splits);
+    dim3 grid(p.mtiles * p.chunks * p.splits);
     RDN_PROBE("wgrad3_rows_kernel<bf16,%d,%d%s>", BM, CK, d->a_gate ? ",gate" : "");
     if (d->a_gate)
       wgrad3_rows_kernel<BM, CK, true><<<grid, NT, 0, st>>>(*d, p.tiles_x, p.tiles_y, p.ntiles, p.tpb);
