@@ -319,10 +319,11 @@ int launch_h(const rdn_conv_desc* d, hipStream_t st) {
 }
 
 // BN choice: 64 for wide outputs (more blocks on the small deep levels; measured
-// best on the L1-L3 shapes), else the candidate minimising padded columns
+// best on the L1-L3 shapes) unless 80 tiles them exactly and 64 does not, else the
+// candidate minimising padded columns
 // ceil(ncols/BN)*BN, ties to the larger BN
 static int pick_bn(int ncols) {
-  if (ncols > 128) return 64;
+  if (ncols > 128) return ncols % 64 && ncols % 80 == 0 ? 80 : 64;   // 160 -> 2 x 80 (measured), else 64
   static const int cands[] = {128, 96, 80, 64, 48, 32, 16};
   int best = 128, waste = 1 << 30;
   for (int b : cands) {

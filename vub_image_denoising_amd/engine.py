@@ -111,6 +111,10 @@ _FLAT_REGISTRY: list = []
 # stop(token); info = (phase, layer, kernel key, algorithmic flops, algorithmic bytes).
 TRACER = None
 
+# PReLU backward is fused into a layer's dgrad/wgrad loaders when its weight-gradient
+# kernel reads the gated operand in at most this many input-channel chunks
+FUSE_MAX_CHUNKS = int(os.environ.get("RDN_FUSE_MAX_CHUNKS", "1"))
+
 
 def find_flat(params):
     """The FlatParams whose parameter list is exactly ``params`` (same objects,
@@ -442,11 +446,11 @@ class UNetEngine:
             # PReLU input); the output conv (NCHW dy) and the 2x2 convs keep
             # the separate rdn_prelu_bwd pass producing dYpre.
             fused = (L.kind == "c3" and L.ddst is not None) and os.environ.get("RDN_FUSE_PRELU", "1") != "0"
-            if fused:  # only when the wgrad reads operand A once (one input-channel chunk)
+            if fused:  # only when the wgrad re-reads operand A (with the gate) at most FUSE_MAX_CHUNKS times
                 n_, h_, w_ = self.grid[L.level]
                 probe = H.WgradDesc(dtype=self.code, gather=H.RDN_G_CONV3, n=n_, h=h_, w=w_, hin=h_, win=w_,
                                     mdim=L.cout, ndim=L.cin_pad)
-                fused = lib.rdn_wgrad_chunks(C.byref(probe)) == 1
+                fused = lib.rdn_wgrad_chunks(C.byref(probe)) <= FUSE_MAX_CHUNKS
             L.extra["fused"] = fused
             pre = self.bufs[L.pre]
             alpha = self.named[L.act + ".weight"]
