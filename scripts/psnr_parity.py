@@ -124,8 +124,9 @@ def run_gpu(args, params, data, dtype):
     with torch.no_grad():
         den = torch.cat([model.improved_sampling(ev_noisy[i:i + args.eval_batch].to(dev)).cpu()
                          for i in range(0, ev_noisy.size(0), args.eval_batch)])
-    return {"psnr": psnr_per_image(den, ev_clean), "loss_first": float(losses[0].item()),
-            "loss_last": float(losses[-1].item()), "train_s": round(t_train, 2)}
+    losses = [float(v) for v in torch.stack(losses).cpu()]
+    return {"psnr": psnr_per_image(den, ev_clean), "loss_first": losses[0], "loss_last": losses[-1],
+            "train_s": round(t_train, 2), "losses": losses}
 
 
 def run_cpu(args, params, data):
@@ -151,7 +152,7 @@ def run_cpu(args, params, data):
         den = torch.cat([R.improved_sampling(fn, ev_noisy[i:i + args.eval_batch], args.timesteps)
                          for i in range(0, ev_noisy.size(0), args.eval_batch)])
     return {"psnr": psnr_per_image(den, ev_clean), "loss_first": losses[0], "loss_last": losses[-1],
-            "train_s": round(t_train, 2), "threads": torch.get_num_threads()}
+            "train_s": round(t_train, 2), "threads": torch.get_num_threads(), "losses": losses}
 
 
 def parser():
@@ -165,30 +166,67 @@ def parser():
     ap.add_argument("--base-filters", type=int, default=32)
     ap.add_argument("--timesteps", type=int, default=20)
     ap.add_argument("--sigma", type=float, default=25.0)
-    ap.add_argument("--lr", type=float, default=1e-3)
+    ap.add_argument("--lr", type=float, default=2e-4)
     ap.add_argument("--seed", type=int, default=2025)
     ap.add_argument("--bf16", action="store_true", help="also train the bf16 build (report only)")
+    ap.add_argument("--seeds", type=int, default=1, help="independent repetitions (PSNR averaged)")
+    ap.add_argument("--self-noise", action="store_true",
+                    help="also train the CPU oracle from ~1e-6-perturbed weights: the protocol's noise floor")
+    ap.add_argument("--keep-losses", action="store_true")
     ap.add_argument("--out", default="")
     return ap
 
 
-def run(args):
+def _one(args, seed):
     from oracle import rdunet_ref as R
     from oracle.weights import make_params
-    params = make_params(R.param_shapes(args.base_filters), args.seed)
-    data = make_data(args)
-    res = {"protocol": "SURVEY.md §8d PSNR@sigma=25: identical init, data and t draws; Adam every step; "
-                       "improved_sampling T=20 on a held-out set; hyperparams_search.py PSNR convention",
-           "config": {k: getattr(args, k) for k in ("steps", "batch", "size", "n_train", "n_eval", "base_filters",
-                                                    "timesteps", "sigma", "lr", "seed")},
-           "psnr_noisy_input": psnr_per_image(data[2], data[3])}
-    res["gpu_fp32"] = run_gpu(args, params, data, "fp32")
-    res["cpu_oracle_fp32"] = run_cpu(args, params, data)
-    res["delta_db"] = res["gpu_fp32"]["psnr"] - res["cpu_oracle_fp32"]["psnr"]
-    res["pass_0p05db"] = bool(abs(res["delta_db"]) <= 0.05)
+    a = argparse.Namespace(**vars(args))
+    a.seed = seed
+    params = make_params(R.param_shapes(a.base_filters), seed)
+    data = make_data(a)
+    r = {"seed": seed, "psnr_noisy_input": psnr_per_image(data[2], data[3])}
+    r["gpu_fp32"] = run_gpu(a, params, data, "fp32")
+    print(f"seed {seed}: gpu fp32 psnr {r['gpu_fp32']['psnr']:.4f}", flush=True)
+    r["cpu_oracle_fp32"] = run_cpu(a, params, data)
+    print(f"seed {seed}: cpu fp32 psnr {r['cpu_oracle_fp32']['psnr']:.4f}", flush=True)
+    if args.self_noise:
+        # the protocol's own noise floor: the same CPU oracle from weights perturbed by
+        # ~1e-6 relative (a few fp32 ulps, the size of GPU-vs-CPU rounding differences)
+        rng = np.random.default_rng(seed + 7)
+        pert = {k: (v * (1 + 1e-6 * rng.standard_normal(v.shape))).astype(np.float32) for k, v in params.items()}
+        r["cpu_oracle_fp32_perturbed"] = run_cpu(a, pert, data)
     if args.bf16:
-        res["gpu_bf16"] = run_gpu(args, params, data, "bf16")
-        res["delta_bf16_vs_fp32_db"] = res["gpu_bf16"]["psnr"] - res["gpu_fp32"]["psnr"]
+        r["gpu_bf16"] = run_gpu(a, params, data, "bf16")
+    lg, lc = r["gpu_fp32"]["losses"], r["cpu_oracle_fp32"]["losses"]
+    rel = [abs(x - y) / abs(y) for x, y in zip(lg, lc)]
+    r["loss_traj_max_rel_diff"] = max(rel)
+    r["loss_traj_first_step_over_1e-3"] = next((i for i, v in enumerate(rel) if v > 1e-3), None)
+    for leg in ("gpu_fp32", "cpu_oracle_fp32", "cpu_oracle_fp32_perturbed", "gpu_bf16"):
+        if leg in r and not args.keep_losses:
+            r[leg].pop("losses")
+    return r
+
+
+def run(args):
+    seeds = [args.seed + 100 * i for i in range(args.seeds)]
+    runs = [_one(args, s) for s in seeds]
+    mean = lambda leg: float(np.mean([r[leg]["psnr"] for r in runs]))
+    res = {"protocol": "SURVEY.md §8d PSNR@sigma=25: identical init, data and t draws; Adam every step; "
+                       "improved_sampling T=20 on a held-out set; hyperparams_search.py PSNR convention; "
+                       "mean over seeds",
+           "config": {k: getattr(args, k) for k in ("steps", "batch", "size", "n_train", "n_eval", "base_filters",
+                                                    "timesteps", "sigma", "lr", "seed", "seeds")},
+           "psnr_noisy_input": float(np.mean([r["psnr_noisy_input"] for r in runs])),
+           "psnr_gpu_fp32": mean("gpu_fp32"), "psnr_cpu_oracle_fp32": mean("cpu_oracle_fp32")}
+    res["delta_db"] = res["psnr_gpu_fp32"] - res["psnr_cpu_oracle_fp32"]
+    res["pass_0p05db"] = bool(abs(res["delta_db"]) <= 0.05)
+    if args.self_noise:
+        res["psnr_cpu_oracle_fp32_perturbed"] = mean("cpu_oracle_fp32_perturbed")
+        res["self_noise_delta_db"] = res["psnr_cpu_oracle_fp32_perturbed"] - res["psnr_cpu_oracle_fp32"]
+    if args.bf16:
+        res["psnr_gpu_bf16"] = mean("gpu_bf16")
+        res["delta_bf16_vs_fp32_db"] = res["psnr_gpu_bf16"] - res["psnr_gpu_fp32"]
+    res["runs"] = runs
     return res
 
 

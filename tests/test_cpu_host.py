@@ -104,3 +104,29 @@ def test_blocks_refuse_standalone_forward():
     import vub_image_denoising_amd as vm
     with pytest.raises(RuntimeError):
         vm.DenoisingBlock(32, 16, 32)(torch.zeros(1, 32, 8, 8))
+
+
+def test_trainer_variants_keep_reference_signatures():
+    """The three reference scripts declare different trainer signatures
+    (diffusion_RDUnet.py:76,117; main_diffusion_RDUnet.py:237,275;
+    diffusion_RDUnet_direct.py:228,266): each drop-in module keeps its own."""
+    import inspect
+    from vub_image_denoising_amd import diffusion_RDUnet as A, diffusion_RDUnet_direct as D, main_diffusion_RDUnet as M
+
+    def names(f):
+        return list(inspect.signature(f).parameters)
+
+    assert names(A.train_step_checkpointed)[:7] == ["model", "clean_images", "noisy_images", "optimizer",
+                                                    "accumulation_steps", "distribution_choice", "clip_value"]
+    assert names(A.train_model_checkpointed)[:8] == ["model", "train_loader", "val_loader", "optimizer", "scheduler",
+                                                     "writer", "output_dir", "distribution_choice"]
+    for mod in (M, D):
+        assert names(mod.train_step_checkpointed) == ["model", "clean_images", "noisy_images", "optimizer",
+                                                      "accumulation_steps", "clip_value"]
+        assert names(mod.train_model_checkpointed) == ["model", "train_loader", "val_loader", "optimizer", "scheduler",
+                                                       "writer", "num_epochs", "start_epoch", "accumulation_steps",
+                                                       "clip_value"]
+        assert names(mod.load_checkpoint) == ["model", "optimizer", "scheduler", "checkpoint_path"]
+    # direct variant: forward = forward_diffusion + direct_sampling (diffusion_RDUnet_direct.py:203-206)
+    assert D.DiffusionModel.forward is not A.DiffusionModel.forward
+    assert issubclass(D.DiffusionModel, A.DiffusionModel)

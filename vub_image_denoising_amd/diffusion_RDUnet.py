@@ -121,6 +121,16 @@ def train_model_checkpointed(model, train_loader, val_loader, optimizer, schedul
     every-``accumulation_steps`` optimizer step, one-batch improved_sampling
     validation, scheduler step and a checkpoint dict per epoch.  ``log_every``
     > 1 rate-limits the per-batch ``loss.item()`` host sync."""
+    run_epochs(model, train_loader, val_loader, optimizer, scheduler, writer, output_dir, distribution_choice,
+               num_epochs, start_epoch, accumulation_steps, clip_value, log_every,
+               sample=lambda m, x: m.improved_sampling(x))
+
+
+def run_epochs(model, train_loader, val_loader, optimizer, scheduler, writer, output_dir, distribution_choice,
+               num_epochs, start_epoch, accumulation_steps, clip_value, log_every, sample):
+    """The epoch loop shared by the three reference trainers (diffusion_RDUnet.py:117-178,
+    main_diffusion_RDUnet.py:275-336, diffusion_RDUnet_direct.py:266-327); they
+    differ only in the validation sampler and the checkpoint directory."""
     dev = next(model.parameters()).device
     for epoch in range(start_epoch, num_epochs):
         model.train()
@@ -143,7 +153,7 @@ def train_model_checkpointed(model, train_loader, val_loader, optimizer, schedul
             with torch.no_grad():
                 val_noisy_images, val_clean_images = next(iter(val_loader))
                 val_noisy_images, val_clean_images = val_noisy_images.to(dev), val_clean_images.to(dev)
-                denoised_images = model.improved_sampling(val_noisy_images)
+                denoised_images = sample(model, val_noisy_images)
                 validation_loss = combined_loss(denoised_images, val_clean_images).item()
         print(f"Epoch [{epoch + 1}/{num_epochs}], Validation Loss: {validation_loss:.4f}")
         if writer is not None:
