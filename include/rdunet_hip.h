@@ -215,6 +215,29 @@ int rdn_nhwc_to_nchw(int32_t dtype, const void* src, int64_t src_ps, int32_t src
 /* fill a [pixels][cols] NHWC slice with zeros */
 int rdn_zero_slice(int32_t dtype, void* dst, int64_t pixels, int64_t ps, int32_t c0, int32_t cols, void* stream);
 
+/* GPU data synthesis: replaces CustomDataset.__getitem__ (dataset_creation/custom_dataset.py:64-100)
+   and CustomSIDD_Dataset.__getitem__ (dataset_creation/SIDD_dataset.py:74-97) + the torchvision
+   transforms of data_loader.py:35-46 for a whole batch.  One item = one P x P patch of a uint8 HWC
+   image resident in device memory. */
+typedef struct rdn_synth_item {
+  int64_t clean_off;   /* byte offset of the patch's (0,0) pixel in clean_pool                  */
+  int64_t noisy_off;   /* same in noisy_pool (real noisy/gt pairs); unused with synthetic noise */
+  uint64_t seed;       /* key of the device noise stream                                       */
+  int32_t row_stride;  /* bytes between two rows of the source image (width * channels)         */
+  float sigma;         /* Gaussian sigma on the 0..255 scale (custom_dataset.py:83-85); 0: none */
+  int32_t flip;        /* RandomHorizontalFlip fired (data_loader.py:42)                        */
+  int32_t rotate;      /* RandomRotation fired: affine[] holds Pillow's 16.16 fixed-point       */
+  int32_t affine[6];   /*   output->input coefficients of Image.rotate(angle, NEAREST) (:43)    */
+} rdn_synth_item;
+/* out_noisy / out_clean: fp32 NCHW [n][channels][patch][patch] in [-1, 1] (ToTensor +
+   Normalize(0.5, 0.5)).  noisy_pool != NULL: the noisy image is read (paired data).  Otherwise
+   noisy = clip(float32(clean + noise)) -> uint8 with noise[n][patch][patch][channels] (float64,
+   e.g. the reference's np.random.normal draws) when noise != NULL, else a counter-based
+   N(0, sigma) draw on the device.  items is a DEVICE array. */
+int rdn_synth_batch(const rdn_synth_item* items, int32_t n, int32_t channels, int32_t patch,
+                    const uint8_t* clean_pool, const uint8_t* noisy_pool, const double* noise,
+                    float* out_noisy, float* out_clean, void* stream);
+
 const char* rdn_version(void);
 const char* rdn_last_error(void);
 

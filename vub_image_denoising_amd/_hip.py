@@ -55,6 +55,11 @@ class PackItem(C.Structure):
                 ("pad0", _i32), ("pad1", _i32), ("rows_pad", _i32), ("kp", _i32), ("ck", _i32)]
 
 
+class SynthItem(C.Structure):
+    _fields_ = [("clean_off", _i64), ("noisy_off", _i64), ("seed", C.c_uint64), ("row_stride", _i32),
+                ("sigma", _f32), ("flip", _i32), ("rotate", _i32), ("affine", _i32 * 6)]
+
+
 # name -> (restype, argtypes); every symbol include/rdunet_hip.h declares
 SIGNATURES = {
     "rdn_conv_fwd": (_i32, [C.POINTER(ConvDesc), _vp]),
@@ -86,6 +91,7 @@ SIGNATURES = {
     "rdn_nchw_to_nhwc": (_i32, [_i32, _vp, _i32, _i32, _i32, _i32, _vp, _i64, _i32, _vp]),
     "rdn_nhwc_to_nchw": (_i32, [_i32, _vp, _i64, _i32, _i32, _i32, _i32, _i32, _vp, _i32, _vp]),
     "rdn_zero_slice": (_i32, [_i32, _vp, _i64, _i64, _i32, _i32, _vp]),
+    "rdn_synth_batch": (_i32, [_vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "rdn_version": (C.c_char_p, []),
     "rdn_last_error": (C.c_char_p, []),
 }
