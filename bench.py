@@ -14,8 +14,15 @@ Prints ONE JSON line (rank 0).  Extra objects:
   roofline      dominant kernel instantiation, achieved algorithmic TFLOP/s or
                 GB/s measured with HIP events on the compute stream over the timed
                 region, against the MI355X peak (MI355X_MICROARCH.md)
+                `traffic`: HBM bytes per launch of that kernel from rocprofv3 PMC
+                counters (FETCH_SIZE x2 + WRITE_SIZE, separate passes of a short
+                child run of this bench; MI355X_MICROARCH.md HBM section)
   cpu_baseline  the CPU oracle (torch fp32 NCHW, the reference's aten math) train
                 step at batch 2 on this host's cores, bounded sample
+  inference     the samplers on the same GPU: improved_sampling latency on one
+                256x256 image (the reference publishes ~1.29 s) and config 4's
+                direct_sampling at batch 64 x 512x512
+Progress goes to stderr.
 """
 from __future__ import annotations
 
@@ -107,6 +114,138 @@ def cpu_baseline(seconds=12.0, batch=2, size=256):
                       f"x 3x{size}x{size}, {el:.1f}s on the host CPU"}
 
 
+def _log(msg):
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def _kernel_sig(name):
+    """(base name, integer template args, gate flag) of a kernel instantiation, from
+    the launch probe's key ('conv3_halo_kernel<bf16,64,2,64,gate>') or from a
+    rocprofv3 kernel name (Itanium-mangled or demangled).  Element types are
+    dropped (one bench run uses one dtype)."""
+    import re
+    if name.startswith("_Z"):
+        end = name.find("_kernelI")
+        if end < 0:
+            return None
+        end += len("_kernel")
+        base = None
+        for start in range(end - 1, 0, -1):     # <length><identifier> ending at `end`
+            n = str(end - start)
+            if name[start - len(n):start] == n and (name[start].isalpha() or name[start] == "_"):
+                base = name[start:end]
+                break
+        if base is None:
+            return None
+        rest, ints, gate = name[end + 1:], [], False
+        while rest and rest[0] != "E":
+            t = re.match(r"DF16b|f|Li(\d+)E|Lb([01])E", rest)
+            if not t:
+                return None
+            if t.group(1) is not None:
+                ints.append(int(t.group(1)))
+            elif t.group(2) is not None:
+                gate = t.group(2) == "1"
+            rest = rest[t.end():]
+        return base, ints, gate
+    m = re.search(r"(\w+_kernel)<([^>]*)>", name)
+    if not m:
+        return None
+    ints, gate = [], False
+    for tok in (x.strip() for x in m.group(2).split(",")):
+        if tok.isdigit():
+            ints.append(int(tok))
+        elif tok in ("gate", "true"):
+            gate = True
+    return m.group(1), ints, gate
+
+
+def pmc_traffic(key, args, timeout=240):
+    """HBM bytes per launch of kernel `key`, from rocprofv3 PMC counters collected
+    in two child runs of this bench (MI355X_MICROARCH.md, HBM section: FETCH_SIZE and
+    WRITE_SIZE in separate --pmc passes beside --kernel-trace only; on gfx950
+    FETCH_SIZE tallies 128-B requests at 64 B, so it is doubled).  Returns
+    (bytes or None, note)."""
+    import csv
+    import glob
+    import shutil
+    import signal
+    import subprocess
+    import tempfile
+    if shutil.which("rocprofv3") is None:
+        return None, "rocprofv3 not on PATH"
+    want = _kernel_sig(key)
+    kb = {}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="rdn_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+        cmd = ["rocprofv3", "--kernel-trace", "--pmc", ctr, "-d", d, "-o", "run", "--output-format", "csv", "--",
+               sys.executable, os.path.abspath(__file__), "--pmc-child", "--no-cpu-baseline", "--steps", "2",
+               "--warmup", "1", "--batch", str(args.batch), "--size", str(args.size), "--base-filters",
+               str(args.base_filters), "--dtype", args.dtype]
+        p = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, start_new_session=True)
+        try:
+            rc = p.wait(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()
+            shutil.rmtree(d, ignore_errors=True)
+            return None, f"{ctr} pass timed out"
+        vals = []
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            with open(f) as fh:
+                for row in csv.DictReader(fh):
+                    if row.get("Counter_Name") == ctr and _kernel_sig(row.get("Kernel_Name", "")) == want:
+                        vals.append(float(row["Counter_Value"]))
+        shutil.rmtree(d, ignore_errors=True)
+        if rc != 0 or not vals:
+            return None, f"{ctr} pass rc={rc}, {len(vals)} matching dispatches"
+        kb[ctr] = sum(vals) / len(vals)
+    return (2.0 * kb["FETCH_SIZE"] + kb["WRITE_SIZE"]) * 1024.0, "rocprofv3 PMC, FETCH_SIZE x2 + WRITE_SIZE, KiB"
+
+
+def inference_bench(dev, base_filters=32):
+    """The sampler paths on the same GPU (hipGraph-captured, SamplerGraph):
+    improved_sampling (2T = 40 UNet forwards, diffusion_RDUnet.py:38-50) on one
+    256x256 image — the reference's published ≈1.29 s/image — and
+    config 4's direct_sampling at batch 64 x 512x512."""
+    import vub_image_denoising_amd as vm
+    from vub_image_denoising_amd.diffusion_RDUnet import DiffusionModel
+    from vub_image_denoising_amd.sampling import SamplerGraph
+    torch.manual_seed(7)
+    dm = DiffusionModel(vm.RDUNet_T(base_filters=base_filters), timesteps=20).to(dev).eval()
+    res = {}
+
+    def timed(fn, reps):
+        fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / reps
+
+    x1 = torch.rand(1, 3, 256, 256, device=dev) * 2 - 1
+    for dt in ("fp32", "bf16"):
+        dm.unet.set_compute_dtype(dt)
+        g = SamplerGraph(dm, tuple(x1.shape))
+        res[f"improved_sampling_256_b1_{dt}_ms"] = round(1e3 * timed(lambda: g(x1), 5), 3)
+        del g
+    res["published_improved_sampling_256_b1_s"] = 1.29
+    res["speedup_vs_published_fp32"] = round(1.29e3 / res["improved_sampling_256_b1_fp32_ms"], 1)
+    dm.unet.set_compute_dtype("bf16")
+    x64 = torch.rand(64, 3, 512, 512, device=dev) * 2 - 1
+    g = SamplerGraph(dm, tuple(x64.shape), direct=True)
+    t = timed(lambda: g(x64), 3)
+    eng = dm.unet._rdn_engines[(64, 512, 512, torch.bfloat16, False)]
+    flops = sum(L.extra["info"]["fwd"][3] for L in eng.layers)
+    res["direct_sampling_512_b64_bf16"] = {"ms_per_call": round(1e3 * t, 2), "images_per_s": round(64 / t, 1),
+                                           "tflops": round(flops / t / 1e12, 1)}
+    del g, x64
+    dm.unet._rdn_engines.clear()
+    torch.cuda.empty_cache()
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -119,6 +258,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--layer-report", default="", help="write a per-kernel time table (json) here")
+    ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes (roofline.traffic)")
+    ap.add_argument("--no-inference", action="store_true", help="skip the sampler measurements")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -225,11 +367,26 @@ def main():
                     "unit": "GB/s"}
         roof["frac"] = round(roof["achieved"] / roof["peak"], 4)
         roof["traffic"] = None
+        if not (args.no_traffic or args.pmc_child) and world == 1:
+            _log(f"PMC traffic passes for {dom}")
+            traffic, note = pmc_traffic(dom, args)
+            if traffic is not None:
+                roof["traffic"] = round(traffic / 1e6, 3)
+                roof["traffic_unit"] = "MB per launch"
+                roof["algorithmic_bytes_mb"] = round(bytes_per / 1e6, 3)
+                roof["traffic_over_algorithmic"] = round(traffic / bytes_per, 3)
+            roof["traffic_source"] = note
         roof["kernel"] = dom
         roof["avg_launch_us"] = round(avg_ms * 1e3, 2)
         roof["launches_per_step"] = d["n"] // args.steps
         roof["share_of_step"] = round(d["ms"] / (el * 1e3), 4)
-        cpu = None if args.no_cpu_baseline else cpu_baseline(args.cpu_seconds)
+        if not (args.no_cpu_baseline or args.pmc_child):
+            _log("CPU baseline")
+        cpu = None if (args.no_cpu_baseline or args.pmc_child) else cpu_baseline(args.cpu_seconds)
+        infer = None
+        if not (args.no_inference or args.pmc_child) and world == 1:
+            _log("sampler measurements")
+            infer = inference_bench(dev, args.base_filters)
         out = {
             "metric": "images/sec (256x256x3) RDUNet diffusion train step",
             "value": round(images / el, 2),
@@ -251,6 +408,7 @@ def main():
                        "final_loss": round(loss_v, 5)},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "inference": infer,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
