@@ -45,9 +45,9 @@ def test_plan_buckets_cover_everything_once():
     assert any(hi - lo >= 900000 for lo, hi in covered)
 
 
-def _worker(rank, world, port, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _worker(rank, world, init_file, q):
+    # file:// rendezvous: no TCP port to race for between parallel test runs
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
     try:
         fp = _fake_flat(100 + rank, SIZES)
         mine = fp.gflat.clone()
@@ -72,11 +72,11 @@ def _free_port():
     return p
 
 
-def test_gradsync_world2_gloo_average():
+def test_gradsync_world2_gloo_average(tmp_path):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    init_file = str(tmp_path / "rendezvous")
+    procs = [ctx.Process(target=_worker, args=(r, 2, init_file, q)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict()

@@ -1,0 +1,72 @@
+"""Data-parallel training through the real network on the GPU: two ranks (gloo
+over the one GPU of the box; the 8-GPU RCCL run is the driver's), each training on
+half of a batch with ddp.GradSync attached (bucketed all-reduce on a side stream,
+overlapped with the fused backward), must end with the clipped gradient the single
+process computes on the whole batch: images are
+independent and the loss is a mean over equal halves."""
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(seed=41):
+    from oracle.weights import make_params
+    import vub_image_denoising_amd as vm
+    from vub_image_denoising_amd.diffusion_RDUnet import DiffusionModel
+    model = DiffusionModel(vm.RDUNet_T(base_filters=16), timesteps=20)
+    sd = model.state_dict()
+    p = make_params({k[5:]: tuple(v.shape) for k, v in sd.items()}, seed)
+    model.load_state_dict({"unet." + k: torch.from_numpy(v) for k, v in p.items()})
+    g = torch.Generator().manual_seed(5)
+    clean = torch.rand(4, 3, 32, 32, generator=g) * 2 - 1
+    noisy = clean + 0.2 * torch.randn(4, 3, 32, 32, generator=g)
+    t = torch.tensor([3, 11, 17, 20])
+    return model.cuda(), clean.cuda(), noisy.cuda(), t.cuda()
+
+
+def _rank(rank, world, init_file, q):
+    try:
+        dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+        from vub_image_denoising_amd.ddp import GradSync
+        from vub_image_denoising_amd.diffusion_RDUnet import train_step_device
+        model, clean, noisy, t = _setup()
+        opt = torch.optim.SGD(model.parameters(), lr=0.0)
+        sl = slice(2 * rank, 2 * rank + 2)
+        train_step_device(model, clean[sl], noisy[sl], opt, clip_value=1.0, t=t[sl])  # builds the flat buffer
+        model.unet._rdn_flat.grad_sync = GradSync(model.unet._rdn_flat, bucket_mb=0.5)
+        train_step_device(model, clean[sl], noisy[sl], opt, clip_value=1.0, t=t[sl])
+        torch.cuda.synchronize()
+        q.put((rank, model.unet._rdn_flat.gflat.cpu().numpy(), len(model.unet._rdn_flat.grad_sync.buckets)))
+        dist.destroy_process_group()
+    except Exception as e:  # report instead of hanging the parent on q.get
+        q.put((rank, repr(e), 0))
+
+
+def test_ddp_two_ranks_match_single_process(tmp_path):
+    from vub_image_denoising_amd.diffusion_RDUnet import train_step_device
+    model, clean, noisy, t = _setup()
+    opt = torch.optim.SGD(model.parameters(), lr=0.0)
+    train_step_device(model, clean, noisy, opt, clip_value=1.0, t=t)
+    torch.cuda.synchronize()
+    ref = model.unet._rdn_flat.gflat.cpu().numpy()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank, args=(r, 2, str(tmp_path / "rdv"), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        r, g, nb = q.get(timeout=110)
+        assert not isinstance(g, str), g
+        res[r] = (g, nb)
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    assert res[0][1] > 1, "several buckets (launched during the backward)"
+    assert np.array_equal(res[0][0], res[1][0]), "ranks hold the same averaged gradient"
+    err = np.linalg.norm(res[0][0] - ref) / np.linalg.norm(ref)
+    assert err < 1e-5, err
