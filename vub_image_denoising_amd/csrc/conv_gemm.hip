@@ -190,6 +190,74 @@ __global__ __launch_bounds__(NT) void conv_gemm_kernel(rdn_conv_desc d, FastDiv 
   const int flags = d.flags;
   const int H = d.h, W = d.w;
   constexpr int UPR = BN / VEC;
+  // fast epilogue: a thread's 16-B column unit is fixed (NT % UPR == 0), so bias /
+  // PReLU slope / scatter tap are loaded and decoded once, and every access is a
+  // whole 16-B NHWC unit
+  static_assert(NT % UPR == 0, "fixed column unit per thread");
+  const bool fast = (d.ncols % VEC) == 0 && !(flags & RDN_EPI_OUT_NCHW) && d.out_ps % VEC == 0 &&
+                    d.out_c0 % VEC == 0 && d.pre_ps % VEC == 0 &&
+                    (!(flags & RDN_EPI_RESID) || (d.res_climit % VEC == 0 && d.res_ps % VEC == 0 &&
+                                                  d.res_c0 % VEC == 0));
+  if (fast) {
+    constexpr int RPI = NT / UPR;              // tile rows per pass
+    const int cu = tid % UPR;
+    const int col = n0 + cu * VEC;
+    if (col >= d.ncols) return;
+    int c = col, tp = 0;
+    if (flags & RDN_EPI_SCATTER2) { tp = col / d.cout; c = col - tp * d.cout; }
+    float eb[VEC], ea[VEC];
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) {
+      eb[q] = (flags & RDN_EPI_BIAS) ? d.bias[c + q] : 0.f;
+      ea[q] = (flags & RDN_EPI_PRELU) ? d.alpha[c + q] : 0.f;
+    }
+    const bool resid = (flags & RDN_EPI_RESID) && c < d.res_climit;
+#pragma unroll 2
+    for (int r = tid / UPR; r < BM; r += RPI) {
+      const int64_t m = m0 + r;
+      if (m >= M) break;
+      int64_t opix = m;
+      if (flags & RDN_EPI_SCATTER2) {
+        const int nimg = (int)fdiv((uint32_t)m, fd_hw);
+        const int rem = (int)m - nimg * H * W;
+        const int y = (int)fdiv((uint32_t)rem, fd_w);
+        const int x = rem - y * W;
+        opix = ((int64_t)nimg * (2 * H) + 2 * y + (tp >> 1)) * (2 * W) + 2 * x + (tp & 1);
+      }
+      float v[VEC];
+      const float* src = Ct + r * CROW + cu * VEC;
+#pragma unroll
+      for (int q = 0; q < VEC; q += 4) {
+        const f32x4 t4 = *(const f32x4*)(src + q);
+        v[q] = t4[0]; v[q + 1] = t4[1]; v[q + 2] = t4[2]; v[q + 3] = t4[3];
+      }
+      if (flags & RDN_EPI_BIAS) {
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) v[q] += eb[q];
+      }
+      if (flags & RDN_EPI_STORE_PRE) *(u32x4*)((T*)d.pre + opix * d.pre_ps + c) = Unit16<T>::pack(v);
+      if (flags & RDN_EPI_PRELU) {
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) v[q] = v[q] > 0.f ? v[q] : ea[q] * v[q];
+      }
+      T* const op = (T*)d.out + opix * d.out_ps + d.out_c0 + c;
+      if (resid || (flags & RDN_EPI_ACCUM)) {
+        float rv[VEC];
+        if (resid) {
+          Unit16<T>::unpack(*(const u32x4*)((const T*)d.res + opix * d.res_ps + d.res_c0 + c), rv);
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) v[q] += rv[q];
+        }
+        if (flags & RDN_EPI_ACCUM) {
+          Unit16<T>::unpack(*(const u32x4*)op, rv);
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) v[q] += rv[q];
+        }
+      }
+      *(u32x4*)op = Unit16<T>::pack(v);
+    }
+    return;
+  }
 #pragma nounroll
   for (int u = tid; u < BM * UPR; u += NT) {
     const int r = u / UPR, cu = u - r * UPR;
