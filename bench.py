@@ -50,16 +50,18 @@ class EventTracer:
         self.keys = keys      # None = every traced launch
         self.records = []     # (info, start, end)
 
-    def start(self, info):
+    def start(self, info, stream=None):
+        """Events go on the stream the traced kernel is launched on (the
+        engine's weight-gradient side stream for wgrad launches)."""
         if self.keys is not None and info[2] not in self.keys:
             return None
         s = torch.cuda.Event(enable_timing=True)
-        s.record()
-        return (info, s)
+        s.record(stream)
+        return (info, s, stream)
 
     def stop(self, tok):
         e = torch.cuda.Event(enable_timing=True)
-        e.record()
+        e.record(tok[2])
         self.records.append((tok[0], tok[1], e))
 
     def per_layer(self):

@@ -81,24 +81,25 @@ class GradSync:
         self._remaining = list(self.counts)
         self._launched = [False] * len(self.buckets)
 
-    def params_done(self, indices):
-        """The gradients of these parameter indices are final on the compute
-        stream; launch every bucket that just became complete.  Every rank runs
-        the same backward, so buckets are issued in the same order everywhere."""
+    def params_done(self, indices, stream=None):
+        """The gradients of these parameter indices are final on ``stream`` (the
+        engine's weight-gradient stream; default: the current stream); launch
+        every bucket that just became complete.  Every rank runs the same
+        backward, so buckets are issued in the same order everywhere."""
         for i in indices:
             b = self.param_bucket[i]
             self._remaining[b] -= 1
             if self._remaining[b] == 0:
-                self._launch(b)
+                self._launch(b, stream)
 
-    def _launch(self, b):
+    def _launch(self, b, src=None):
         if self._launched[b]:
             return
         self._launched[b] = True
         lo, hi = self.buckets[b]
         view = self.fp.gflat[lo:hi]
         if self.overlap:
-            self.stream.wait_stream(torch.cuda.current_stream())
+            self.stream.wait_stream(src if src is not None else torch.cuda.current_stream())
             with torch.cuda.stream(self.stream):
                 self._works.append(dist.all_reduce(view, group=self.group, async_op=True))
         else:

@@ -114,6 +114,10 @@ TRACER = None
 # PReLU backward is fused into a layer's dgrad/wgrad loaders when its weight-gradient
 # kernel reads the gated operand in at most this many input-channel chunks
 FUSE_MAX_CHUNKS = int(os.environ.get("RDN_FUSE_MAX_CHUNKS", "1"))
+# weight gradients on a side stream (overlapped with the dgrad chain) and the depth
+# of the dYpre ring that decouples the two chains
+WGRAD_STREAM = os.environ.get("RDN_WGRAD_STREAM", "1") != "0"
+WGRAD_SLOTS = max(2, int(os.environ.get("RDN_WGRAD_SLOTS", "4")))
 
 
 def find_flat(params):
@@ -372,12 +376,16 @@ class UNetEngine:
                 if name.startswith("PRE_"):
                     continue
                 self.bufs["d" + name] = torch.zeros(self.P[lvl], ch, dtype=dtype, device=dev)
-            dyp = max(self.P[self._out_level(L)] * L.cout_pad for L in layers)
-            self.dyp = torch.zeros(dyp, dtype=dtype, device=dev)
+            # weight gradients (wgrad + reduce) run on a side stream, overlapped with
+            # the dgrad chain; the per-layer dYpre / PReLU-partial buffers they read
+            # form a ring of SLOTS so the dgrad chain can run SLOTS layers ahead
+            self.side = torch.cuda.Stream(device=dev) if (dev.type == "cuda" and WGRAD_STREAM) else None
+            self.slots = WGRAD_SLOTS if self.side is not None else 1
+            self.dyp_elems = max(self.P[self._out_level(L)] * L.cout_pad for L in layers)
+            self.dyp = torch.zeros(self.slots, self.dyp_elems, dtype=dtype, device=dev)
             lib = H.lib()
-            pws = max(lib.rdn_prelu_bwd_workspace_size(self.code, self.P[self._out_level(L)], L.cout, L.cout_pad)
-                      for L in layers)
-            self.pws = torch.zeros(max(pws // 4, 4), dtype=torch.float32, device=dev)
+            self.pws_bytes = max(lib.rdn_prelu_bwd_workspace_size(self.code, self.P[self._out_level(L)], L.cout,
+                                                                  L.cout_pad) for L in layers)
             self._build_bwd()
         self._build_info()
         self.token = 0
@@ -439,8 +447,12 @@ class UNetEngine:
         lib = H.lib()
         ws_need = 0
         part_need = 0
+        for b, L in enumerate(reversed(self.layers)):   # backward order -> ring slot
+            L.extra["slot"] = b % self.slots
+            L.extra["dyp"] = self.dyp[L.extra["slot"]].data_ptr()
         for L in self.layers:
             olvl = self._out_level(L)
+            dyp = L.extra["dyp"]
             # 3x3 convs whose output gradient arrives as an NHWC slice run the
             # PReLU backward inside their dgrad / wgrad loaders (gate = saved
             # PReLU input); the output conv (NCHW dy) and the 2x2 convs keep
@@ -459,7 +471,7 @@ class UNetEngine:
             d.dtype = self.code
             packed = L.pack_dgrad[8]
             d.wp, d.kp = packed.data_ptr(), packed.shape[1]
-            d.x, d.x_c0 = self.dyp.data_ptr(), 0
+            d.x, d.x_c0 = dyp, 0
             flags = 0
             if L.kind == "c3":
                 n, h, w = self.grid[L.level]
@@ -499,7 +511,7 @@ class UNetEngine:
                 n, h, w = self.grid[L.level]
                 wg.gather, wg.n, wg.h, wg.w, wg.hin, wg.win = H.RDN_G_CONV3, n, h, w, h, w
                 src = self._buf(L.src.buf)
-                wg.a, wg.a_ps, wg.a_c0, wg.mdim = self.dyp.data_ptr(), L.cout_pad, 0, L.cout
+                wg.a, wg.a_ps, wg.a_c0, wg.mdim = dyp, L.cout_pad, 0, L.cout
                 wg.b, wg.b_ps, wg.b_c0, wg.ndim = src.data_ptr(), src.shape[1], L.src.c0, L.cin_pad
                 taps, ndim_real = 9, L.cin
                 if fused:
@@ -510,7 +522,7 @@ class UNetEngine:
                 n, h, w = self.grid[L.level]
                 wg.gather, wg.n, wg.h, wg.w, wg.hin, wg.win = H.RDN_G_S2, n, h, w, 2 * h, 2 * w
                 src = self._buf(L.src.buf)
-                wg.a, wg.a_ps, wg.a_c0, wg.mdim = self.dyp.data_ptr(), L.cout, 0, L.cout
+                wg.a, wg.a_ps, wg.a_c0, wg.mdim = dyp, L.cout, 0, L.cout
                 wg.b, wg.b_ps, wg.b_c0, wg.ndim = src.data_ptr(), src.shape[1], L.src.c0, L.cin
                 taps, ndim_real = 4, L.cin
             else:
@@ -518,7 +530,7 @@ class UNetEngine:
                 wg.gather, wg.n, wg.h, wg.w, wg.hin, wg.win = H.RDN_G_S2, n, h, w, 2 * h, 2 * w
                 src = self._buf(L.src.buf)
                 wg.a, wg.a_ps, wg.a_c0, wg.mdim = src.data_ptr(), src.shape[1], L.src.c0, L.cin
-                wg.b, wg.b_ps, wg.b_c0, wg.ndim = self.dyp.data_ptr(), L.cout, 0, L.cout
+                wg.b, wg.b_ps, wg.b_c0, wg.ndim = dyp, L.cout, 0, L.cout
                 taps, ndim_real = 4, L.cout
             wg.splits = 0
             splits = lib.rdn_wgrad_splits(C.byref(wg))
@@ -534,12 +546,19 @@ class UNetEngine:
             L.extra["olvl"] = olvl
             L.extra["pidx"] = [self.fp.names.index(n) for n in (L.name + ".weight", L.name + ".bias", L.act + ".weight")]
         self.ws = torch.zeros(max(ws_need // 4, 4), dtype=torch.float32, device=self.device)
-        if part_need > self.pws.numel() * 4:
-            self.pws = torch.zeros(part_need // 4, dtype=torch.float32, device=self.device)
+        pws = max(part_need, self.pws_bytes, 16) // 4
+        self.pws = torch.zeros(self.slots, (pws + 3) // 4 * 4, dtype=torch.float32, device=self.device)
         for L in self.layers:
+            L.extra["pws"] = self.pws[L.extra["slot"]].data_ptr()
             L.wgrad_desc.ws = self.ws.data_ptr()
             if L.extra["fused"]:
-                L.wgrad_desc.part = self.pws.data_ptr()
+                L.wgrad_desc.part = L.extra["pws"]
+        if self.side is not None:   # per layer: dYpre ready (compute stream) / slot free (side stream)
+            for L in self.layers:
+                L.extra["ev_ready"] = torch.cuda.Event()
+                L.extra["ev_done"] = torch.cuda.Event()
+            self.ev_begin = torch.cuda.Event()
+            self.ev_end = torch.cuda.Event()
 
     @staticmethod
     def _probe_copy(desc, cls, keep):
@@ -619,6 +638,14 @@ class UNetEngine:
         return y
 
     def backward(self, dy: torch.Tensor, need_dx: bool):
+        """Reverse sweep.  Compute stream: PReLU backward (unfused layers) and the
+        dgrad chain.  Side stream (when enabled): each layer's wgrad + reduce, which
+        only wait for that layer's dYpre (event ``ev_ready``); a layer's unfused
+        PReLU backward waits for the side stream to release its ring slot (the
+        ``ev_done`` of the layer SLOTS earlier in backward order).  Gradient
+        buffers are never aliased (one per activation buffer) and a slice's
+        gradient is complete before its producer layer is reached, so the two
+        chains share nothing else but these slots."""
         if not self.train:
             raise RuntimeError("engine was built without saved activations (no_grad forward)")
         lib, st = H.lib(), H.stream_ptr()
@@ -627,9 +654,17 @@ class UNetEngine:
         if sync is not None:
             sync.begin()
         dy = dy.contiguous()
-        dyp = self.dyp.data_ptr()
+        side = self.side
+        if side is not None:
+            main = torch.cuda.current_stream()
+            sst = side.cuda_stream
+            self.ev_begin.record(main)
+            side.wait_event(self.ev_begin)   # gradients zeroed / accumulated state ready
+        else:
+            sst = st
         tr = TRACER
-        for L in reversed(self.layers):
+        rev = list(reversed(self.layers))
+        for b, L in enumerate(rev):
             info = L.extra["info"]
             olvl = L.extra["olvl"]
             n, h, w = self.grid[olvl]
@@ -637,22 +672,27 @@ class UNetEngine:
             pre = self.bufs[L.pre]
             ga, gb = L.extra["grad_a"], L.extra["grad_b"]
             fused = L.extra["fused"]
+            dyp, pws = L.extra["dyp"], L.extra["pws"]
             # unfused: the PReLU-backward pass leaves its dalpha/dbias partials in
             # pws for this layer's rdn_wgrad_reduce to sum (no finalize launch)
             if fused:
                 rc = 0
-            elif L.ddst is None:
-                rc = lib.rdn_prelu_bwd(self.code, P, n, h, w, L.cout, L.cout_pad, None, 0, 0, dy.data_ptr(),
-                                       pre.data_ptr(), pre.shape[1], self.named[L.act + ".weight"].data_ptr(),
-                                       dyp, None, None, self.pws.data_ptr(), st)
             else:
-                dd = self.bufs[L.ddst.buf]
-                rc = lib.rdn_prelu_bwd(self.code, P, n, h, w, L.cout, L.cout_pad, dd.data_ptr(), dd.shape[1],
-                                       L.ddst.c0, None, pre.data_ptr(), pre.shape[1],
-                                       self.named[L.act + ".weight"].data_ptr(), dyp, None, None,
-                                       self.pws.data_ptr(), st)
+                if side is not None and b >= self.slots:
+                    main.wait_event(rev[b - self.slots].extra["ev_done"])
+                if L.ddst is None:
+                    rc = lib.rdn_prelu_bwd(self.code, P, n, h, w, L.cout, L.cout_pad, None, 0, 0, dy.data_ptr(),
+                                           pre.data_ptr(), pre.shape[1], self.named[L.act + ".weight"].data_ptr(),
+                                           dyp, None, None, pws, st)
+                else:
+                    dd = self.bufs[L.ddst.buf]
+                    rc = lib.rdn_prelu_bwd(self.code, P, n, h, w, L.cout, L.cout_pad, dd.data_ptr(), dd.shape[1],
+                                           L.ddst.c0, None, pre.data_ptr(), pre.shape[1],
+                                           self.named[L.act + ".weight"].data_ptr(), dyp, None, None, pws, st)
             if rc:
                 H.check(rc, f"prelu_bwd[{L.name}]")
+            if side is not None:
+                L.extra["ev_ready"].record(main)
             if L.name != "input_block.conv_1" or need_dx:
                 tok = tr.start(info["dgrad"]) if tr is not None else None
                 rc = lib.rdn_conv_fwd(C.byref(L.dgrad_desc), st)
@@ -660,8 +700,10 @@ class UNetEngine:
                     tr.stop(tok)
                 if rc:
                     H.check(rc, f"dgrad[{L.name}]")
-            tok = tr.start(info["wgrad"]) if tr is not None else None
-            rc = lib.rdn_conv_wgrad(C.byref(L.wgrad_desc), st)
+            if side is not None:
+                side.wait_event(L.extra["ev_ready"])
+            tok = tr.start(info["wgrad"], side) if tr is not None else None
+            rc = lib.rdn_conv_wgrad(C.byref(L.wgrad_desc), sst)
             if tok is not None:
                 tr.stop(tok)
             if rc:
@@ -669,12 +711,17 @@ class UNetEngine:
             splits, mdim, ndim, ndim_real, taps = L.extra["wgrad"]
             part_splits = 0 if fused else lib.rdn_prelu_bwd_blocks(self.code, P, L.cout_pad)
             rc = lib.rdn_wgrad_reduce(self.ws.data_ptr(), splits, mdim, ndim, ndim_real, taps,
-                                      L.extra["grad_w"].data_ptr(), 1, self.pws.data_ptr(), part_splits,
-                                      ga.data_ptr(), gb.data_ptr(), st)
+                                      L.extra["grad_w"].data_ptr(), 1, pws, part_splits,
+                                      ga.data_ptr(), gb.data_ptr(), sst)
             if rc:
                 H.check(rc, f"wgrad_reduce[{L.name}]")
+            if side is not None:
+                L.extra["ev_done"].record(side)
             if sync is not None:
-                sync.params_done(L.extra["pidx"])
+                sync.params_done(L.extra["pidx"], stream=side)
+        if side is not None:
+            self.ev_end.record(side)
+            main.wait_event(self.ev_end)
         if sync is not None:
             sync.finish()
         if not need_dx:
