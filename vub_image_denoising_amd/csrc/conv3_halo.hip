@@ -18,6 +18,8 @@
 //   P[n][chunk*KC + tap*CK + ci],  KC = roundup(9*CK, SK),  SK = 128 B / elem.
 #include "conv3_tile.h"
 
+#include <cstdlib>
+
 namespace {
 
 constexpr int NT = 256;
@@ -322,7 +324,7 @@ int launch_h(const rdn_conv_desc* d, hipStream_t st) {
 // best on the L1-L3 shapes) unless 80 tiles them exactly and 64 does not, else the
 // candidate minimising padded columns
 // ceil(ncols/BN)*BN, ties to the larger BN
-static int pick_bn(int ncols) {
+static int pick_bn_cols(int ncols) {
   if (ncols > 128) return ncols % 64 && ncols % 80 == 0 ? 80 : 64;   // 160 -> 2 x 80 (measured), else 64
   static const int cands[] = {128, 96, 80, 64, 48, 32, 16};
   int best = 128, waste = 1 << 30;
@@ -333,9 +335,29 @@ static int pick_bn(int ncols) {
   return best;
 }
 
+// minimum grid before BN is halved: a 32x32 level-3 layer has only 128 pixel tiles
+// per 16 images, so BN=128 would leave half of the 256 CUs idle (A/B on MI355X,
+// whole train step: 128 blocks 1351, 256 blocks 1338, 512 blocks 1369 img/s)
+static int min_blocks() {
+  static const int v = [] {
+    const char* e = getenv("RDN_MIN_BLOCKS");
+    return e ? atoi(e) : 512;
+  }();
+  return v;
+}
+
+static int pick_bn(int ncols, int64_t tiles) {
+  int bn = pick_bn_cols(ncols);
+  while ((bn == 128 || bn == 64) && ncols % (bn / 2) == 0 &&
+         tiles * ((ncols + bn - 1) / bn) < (int64_t)min_blocks())
+    bn /= 2;
+  return bn;
+}
+
 template <typename T, int CK>
 int launch_bn(const rdn_conv_desc* d, hipStream_t st) {
-  const int bn = d->bn ? d->bn : pick_bn(d->ncols);
+  const int64_t tiles = (int64_t)d->n * ((d->h + c3::TH - 1) / c3::TH) * ((d->w + c3::TW - 1) / c3::TW);
+  const int bn = d->bn ? d->bn : pick_bn(d->ncols, tiles);
   switch (bn) {
     case 16: return launch_h<T, 16, 4, CK>(d, st);
     case 32: return launch_h<T, 32, 4, CK>(d, st);
@@ -379,7 +401,7 @@ extern "C" int rdn_conv3_packed_k(int32_t cin, int32_t dtype) {
   return (kp + 63) / 64 * 64;
 }
 
-extern "C" int rdn_conv3_pick_bn(int32_t ncols) { return pick_bn(ncols); }
+extern "C" int rdn_conv3_pick_bn(int32_t ncols) { return pick_bn_cols(ncols); }
 
 int rdn_conv3_launch(const rdn_conv_desc* d, hipStream_t st) {
   const int ck = rdn_conv3_chunk_impl(d->cin, d->dtype);
