@@ -59,7 +59,9 @@ def _worker(rank, world, init_file, q):
             gs.params_done(idx[i:i + 3])
         assert all(gs._launched), "every bucket launched once its parameters completed"
         gs.finish()
-        q.put((rank, mine, fp.gflat.clone()))
+        # numpy arrays travel by value; a torch tensor would be shared through a
+        # file descriptor whose socket dies with this process (racy FileNotFoundError)
+        q.put((rank, mine.numpy(), fp.gflat.clone().numpy()))
     finally:
         dist.destroy_process_group()
 
@@ -82,7 +84,7 @@ def test_gradsync_world2_gloo_average(tmp_path):
     res = dict()
     for _ in range(2):
         r, mine, synced = q.get(timeout=120)
-        res[r] = (mine, synced)
+        res[r] = (torch.from_numpy(mine), torch.from_numpy(synced))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

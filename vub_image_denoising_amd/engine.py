@@ -66,16 +66,18 @@ class FlatParams:
                 self.views.append(v)
                 self.gviews.append(self.gflat[off:off + p.numel()].view_as(p))
         self.device = device
+        self._ptrs = [v.data_ptr() for v in self.views]
+        self._gptrs = [g.data_ptr() for g in self.gviews]
         self.generation = 0
         self.grad_sync = None   # ddp.GradSync attached by data-parallel training
         _FLAT_REGISTRY[:] = [r for r in _FLAT_REGISTRY if r() is not None]
         _FLAT_REGISTRY.append(weakref.ref(self))
 
     def intact(self) -> bool:
-        for p, v in zip(self.params, self.views):
-            if p.data.data_ptr() != v.data_ptr() or p.data.dtype != torch.float32:
-                return False
-        return True
+        """Every parameter's storage is still its view of ``flat`` (host-cheap:
+        one pointer list compare; runs several times per training step)."""
+        f32 = torch.float32
+        return [p.data_ptr() for p in self.params] == self._ptrs and all(p.dtype is f32 for p in self.params)
 
     def version_key(self):
         return (self.generation, sum(p._version for p in self.params))
@@ -99,10 +101,10 @@ class FlatParams:
                 p.grad = g
 
     def grads_are_views(self) -> bool:
-        for p, g in zip(self.params, self.gviews):
-            if p.grad is None or p.grad.data_ptr() != g.data_ptr():
-                return False
-        return True
+        grads = [p.grad for p in self.params]
+        if any(g is None for g in grads):
+            return False
+        return [g.data_ptr() for g in grads] == self._gptrs
 
 
 _FLAT_REGISTRY: list = []
