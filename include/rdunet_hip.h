@@ -31,6 +31,10 @@
  *   rdn_sqnorm / rdn_clip_scale  torch.nn.utils.clip_grad_norm_, diffusion_RDUnet.py:113.
  *   rdn_adam_step     torch.optim.Adam / AdamW step, diffusion_RDUnet.py:264-268,127.
  *   rdn_sampling_combine  the x_t update of improved_sampling, diffusion_RDUnet.py:45-49.
+ *   rdn_synth_batch   CustomDataset/CustomSIDD_Dataset.__getitem__ + transforms
+ *                     (dataset_creation/custom_dataset.py:64-100, SIDD_dataset.py:74-97).
+ *   rdn_image_metrics skimage peak_signal_noise_ratio / structural_similarity,
+ *                     evaluate_SIDD/evaluate_SIDD.py:63-64.
  */
 #ifndef RDUNET_HIP_H
 #define RDUNET_HIP_H
@@ -237,6 +241,15 @@ typedef struct rdn_synth_item {
 int rdn_synth_batch(const rdn_synth_item* items, int32_t n, int32_t channels, int32_t patch,
                     const uint8_t* clean_pool, const uint8_t* noisy_pool, const double* noise,
                     float* out_noisy, float* out_clean, void* stream);
+
+/* SIDD evaluation metrics (evaluate_SIDD/evaluate_SIDD.py:63-64, scikit-image 0.22
+   peak_signal_noise_ratio / structural_similarity(channel_axis, win_size 7, uniform
+   window, sample covariance)) for a batch of n fp32 NCHW image pairs: psnr[n] and
+   ssim[n] (float64, device; either may be NULL).  ws: rdn_image_metrics_workspace_size
+   bytes.  Images must be at least 7x7. */
+int64_t rdn_image_metrics_workspace_size(int32_t n, int32_t c, int32_t h, int32_t w);
+int rdn_image_metrics(const float* gt, const float* x, int32_t n, int32_t c, int32_t h, int32_t w,
+                      float data_range, double* ws, double* psnr, double* ssim, void* stream);
 
 const char* rdn_version(void);
 const char* rdn_last_error(void);

@@ -92,6 +92,8 @@ SIGNATURES = {
     "rdn_nhwc_to_nchw": (_i32, [_i32, _vp, _i64, _i32, _i32, _i32, _i32, _i32, _vp, _i32, _vp]),
     "rdn_zero_slice": (_i32, [_i32, _vp, _i64, _i64, _i32, _i32, _vp]),
     "rdn_synth_batch": (_i32, [_vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "rdn_image_metrics_workspace_size": (_i64, [_i32, _i32, _i32, _i32]),
+    "rdn_image_metrics": (_i32, [_vp, _vp, _i32, _i32, _i32, _i32, C.c_float, _vp, _vp, _vp, _vp]),
     "rdn_version": (C.c_char_p, []),
     "rdn_last_error": (C.c_char_p, []),
 }

@@ -120,6 +120,8 @@ FUSE_MAX_CHUNKS = int(os.environ.get("RDN_FUSE_MAX_CHUNKS", "1"))
 # of the dYpre ring that decouples the two chains
 WGRAD_STREAM = os.environ.get("RDN_WGRAD_STREAM", "1") != "0"
 WGRAD_SLOTS = max(2, int(os.environ.get("RDN_WGRAD_SLOTS", "4")))
+# bench.py's per-kernel profiling pass serialises the backward (isolated kernel times)
+SERIAL_BWD = False
 
 
 def find_flat(params):
@@ -656,7 +658,7 @@ class UNetEngine:
         if sync is not None:
             sync.begin()
         dy = dy.contiguous()
-        side = self.side
+        side = None if SERIAL_BWD else self.side
         if side is not None:
             main = torch.cuda.current_stream()
             sst = side.cuda_stream
