@@ -21,6 +21,8 @@
 // contribute nothing.  Splits are summed by rdn_wgrad_reduce (fixed order).
 #include "rdn_common.h"
 
+#include <cstdlib>
+
 namespace {
 
 constexpr int NT = 256;
@@ -548,7 +550,15 @@ Plan plan(const rdn_wgrad_desc* d) {
   p.tiles_y = (d->h + TH - 1) / TH;
   p.ntiles = d->n * p.tiles_x * p.tiles_y;
   const int base = p.mtiles * p.chunks;
-  int s = d->splits > 0 ? d->splits : (512 + base - 1) / base;     // ~2 blocks per CU
+  // blocks per launch (RDN_WGRAD_BLOCKS): one per CU.  The weight gradients run on
+  // the side stream beside the dgrad chain, where fewer, longer blocks (and half
+  // the split-K slab bytes) won: whole step 1342 (512) -> 1362 (256) img/s; 128:
+  // 1165, 192: 1302, 384: 1355, 1024: 1311
+  static const int target = [] {
+    const char* e = getenv("RDN_WGRAD_BLOCKS");
+    return e && atoi(e) > 0 ? atoi(e) : 256;
+  }();
+  int s = d->splits > 0 ? d->splits : (target + base - 1) / base;
   const int maxs = (p.ntiles + 3) / 4;                             // >= 4 tiles per block
   if (s > maxs) s = maxs;
   if (s < 1) s = 1;
