@@ -92,8 +92,45 @@ __global__ __launch_bounds__(256) void prelu_bwd_kernel(int64_t pixels, int H, i
     const int c = grp * VEC + k;
     al[k] = (active && c < C) ? alpha[c] : 0.f;
   }
+  const int64_t stride = (int64_t)gridDim.x * ppb;
+  int64_t p0 = (int64_t)blockIdx.x * ppb + pl;
+#ifndef RDN_NO_PRELU_UNROLL
+  // NHWC fast path: 4 pixel iterations per trip with all 8 loads issued first
+  // (unconditional, from a clamped valid pixel) -- the plain loop exposes one
+  // HBM round trip per pixel, which is what the small level-2/3 passes pay
+  if (active && !dy_nchw && ((dy_ps | dy_c0) % VEC) == 0) {
+    for (; p0 < pixels; p0 += 4 * stride) {
+      u32x4 gv[4], xv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t pu = p0 + u * stride;
+        const int64_t pc = pu < pixels ? pu : p0;
+        gv[u] = *(const u32x4*)(dy + pc * dy_ps + dy_c0 + grp * VEC);
+        xv[u] = *(const u32x4*)(pre + pc * pre_ps + grp * VEC);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t pu = p0 + u * stride;
+        if (pu >= pixels) break;
+        float g[VEC], x[VEC], o[VEC];
+        Unit16<T>::unpack(gv[u], g);
+        Unit16<T>::unpack(xv[u], x);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+          const int c = grp * VEC + k;
+          const bool valid = c < C;
+          const bool pos = x[k] > 0.f;
+          o[k] = valid ? (pos ? g[k] : al[k] * g[k]) : 0.f;
+          if (valid && !pos) sa[k] += x[k] * g[k];
+          sb[k] += o[k];
+        }
+        *(u32x4*)(dyp + pu * cpad + grp * VEC) = Unit16<T>::pack(o);
+      }
+    }
+  }
+#endif
   if (active) {
-    for (int64_t p = (int64_t)blockIdx.x * ppb + pl; p < pixels; p += (int64_t)gridDim.x * ppb) {
+    for (int64_t p = p0; p < pixels; p += stride) {
       float g[VEC], x[VEC], o[VEC];
       if (dy_nchw) {
         const int64_t hw = (int64_t)H * W;
