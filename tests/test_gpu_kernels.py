@@ -467,3 +467,35 @@ def test_conv3_ws_matches_halo(cin, cout, Cs_in, gate, accum):
     else:
         ref = F.prelu(ref, a.cpu()) + _nchw(res, N, Hh, Ww, 0, cout)[:1]
     assert _rel(_nchw(outs[0][0], N, Hh, Ww, 0, cout)[:1], ref) < 2e-2
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_conv3_halo_bn_choice_bit_exact(dt):
+    """The halo kernel's BN (columns per block; grid-aware choice in pick_bn) only
+    changes which block computes a column: outputs are bit-identical for every BN,
+    on a level-3-like shape (128 output channels, 8x16 tiles)."""
+    N, Hh, Ww, cin, cout = 2, 16, 32, 256, 128
+    code = H.dtype_code(dt)
+    x = torch.randn(N * Hh * Ww, cin, device="cuda").to(dt)
+    w = torch.randn(cout, cin, 3, 3, device="cuda") * 0.05
+    b = torch.randn(cout, device="cuda") * 0.1
+    a = torch.full((cout,), 0.25, device="cuda")
+    wp = _pack(H.PACK_CONV_FWD, w, cout, cin, 3, 3, 0, cin, cout, 9 * cin, dt)
+    outs = []
+    for bn in (128, 64, 32):
+        out = torch.zeros(N * Hh * Ww, cout, dtype=dt, device="cuda")
+        pre = torch.zeros_like(out)
+        d = H.ConvDesc(dtype=code, gather=H.RDN_G_CONV3, flags=H.EPI_BIAS | H.EPI_PRELU | H.EPI_STORE_PRE,
+                       n=N, h=Hh, w=Ww, hin=Hh, win=Ww, cin=cin, x=x.data_ptr(), x_ps=cin, x_c0=0,
+                       wp=wp.data_ptr(), kp=wp.shape[1], ncols=cout, cout=cout, bias=b.data_ptr(),
+                       alpha=a.data_ptr(), out=out.data_ptr(), out_ps=cout, out_c0=0, pre=pre.data_ptr(),
+                       pre_ps=cout, bn=bn)
+        H.check(H.lib().rdn_conv_fwd(C.byref(d), H.stream_ptr()), f"conv bn={bn}")
+        torch.cuda.synchronize()
+        outs.append((out.clone(), pre.clone()))
+    for o, p in outs[1:]:
+        assert torch.equal(o, outs[0][0]) and torch.equal(p, outs[0][1])
+    wr = w.cpu().to(dt).float() if dt != torch.float32 else w.cpu()
+    ref = F.conv2d(x.float().cpu().reshape(N, Hh, Ww, cin).permute(0, 3, 1, 2), wr, b.cpu(), padding=1)
+    got = outs[0][1].float().cpu().reshape(N, Hh, Ww, cout).permute(0, 3, 1, 2)
+    assert _rel(got, ref) < _tol(dt)
