@@ -307,12 +307,14 @@ __global__ __launch_bounds__(NT, 2) void wgrad3_rows_kernel(rdn_wgrad_desc d, in
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, g = lane >> 4;
-  // 1-D grid, logical (m-tile, chunk, split) with the m-tile fastest.  With one
-  // block per split, consecutive splits (adjacent pixel ranges: shared halo rows)
-  // go to one XCD (xcd_remap); with several blocks per split the plain order
-  // measured faster (scripts/kbench.py, L1-L3 shapes)
+  // 1-D grid, logical (m-tile, chunk, split) with the m-tile fastest, remapped so
+  // that consecutive logical blocks share an XCD (xcd_remap): the chunks and
+  // m-tiles of one pixel range then read its dY / X tiles through ONE L2.  With
+  // the plain order they spread over all 8 XCDs: level-2/3 wgrad HBM traffic
+  // 195 MB -> 74 MB per launch (PMC, 4.0x -> 1.5x the algorithmic bytes) at the
+  // same step time beside the dgrad chain (isolated the plain order was faster)
   const int mtiles = (d.mdim + BM - 1) / BM, nchunks = d.ndim / CK;
-  const int lb = mtiles * nchunks == 1 ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
   const int bx = lb % mtiles, by = (lb / mtiles) % nchunks, bz = lb / (mtiles * nchunks);
   const int m0 = bx * BM;
   const int c0 = by * CK;
