@@ -285,7 +285,7 @@ __global__ __launch_bounds__(NT, 2) void wgrad3_halo_kernel(rdn_wgrad_desc d, in
 // fixed for the launch plus an immediate, and the tile loaders add one
 // precomputed per-unit offset to a per-tile base.
 template <int BM, int CK, bool GATE>
-__global__ __launch_bounds__(NT, 2) void wgrad3_rows_kernel(rdn_wgrad_desc d, int tiles_x, int tiles_y, int ntiles,
+__global__ __launch_bounds__(NT, (BM * CK > 2560 ? 1 : 2)) void wgrad3_rows_kernel(rdn_wgrad_desc d, int tiles_x, int tiles_y, int ntiles,
                                                             int tiles_per_block) {
   constexpr int VEC = 8;
   constexpr int NCOL = 9 * CK;
@@ -361,8 +361,8 @@ __global__ __launch_bounds__(NT, 2) void wgrad3_rows_kernel(rdn_wgrad_desc d, in
     }
   }
 
-  u32x4 dreg[D_IT], greg[GATE ? D_IT : 1], hreg[H_IT];
-  auto load_tile = [&](int t) {
+  constexpr int GD = GATE ? D_IT : 1;
+  auto load_tile = [&](int t, u32x4 (&dreg)[D_IT], u32x4 (&greg)[GD], u32x4 (&hreg)[H_IT]) {
     const int tx = t % tiles_x, r1 = t / tiles_x;
     const int ty = r1 % tiles_y, nimg = r1 / tiles_y;
     const int y0 = ty * TH, x0 = tx * TW;
@@ -399,7 +399,7 @@ __global__ __launch_bounds__(NT, 2) void wgrad3_rows_kernel(rdn_wgrad_desc d, in
       hreg[it] = v;
     }
   };
-  auto store_tile = [&]() {
+  auto store_tile = [&](const u32x4 (&dreg)[D_IT], const u32x4 (&greg)[GD], const u32x4 (&hreg)[H_IT]) {
 #pragma unroll
     for (int it = 0; it < D_IT; ++it) {
       if (it + 1 == D_IT && tid + it * NT >= D_UNITS) continue;
@@ -449,13 +449,8 @@ __global__ __launch_bounds__(NT, 2) void wgrad3_rows_kernel(rdn_wgrad_desc d, in
     boff[j] = ((tp / 3) * (TW + 2) + tp % 3) * HROW + ci * 2;
   }
 
-  if (t_beg < t_end) {
-    load_tile(t_beg);
-    store_tile();
-  }
-  __syncthreads();
-  for (int t = t_beg; t < t_end; ++t) {
-    if (t + 1 < t_end) load_tile(t + 1);
+  auto compute_tile = [&]() {
+    __builtin_amdgcn_sched_barrier(0);   // keep each tile's fragment reads inside its own phase
 #pragma unroll
     for (int ks = 0; ks < TP / 32; ++ks) {
       bf16x8 af[MT];
@@ -477,12 +472,52 @@ __global__ __launch_bounds__(NT, 2) void wgrad3_rows_kernel(rdn_wgrad_desc d, in
         for (int i = 0; i < MT; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][j], 0, 0, 0);
       }
     }
+  };
+
+  u32x4 dA[D_IT], gA[GD], hA[H_IT];
+#ifndef RDN_WROWS_PF2
+  // one tile in flight: load t+1 during tile t's MFMAs
+  if (t_beg < t_end) {
+    load_tile(t_beg, dA, gA, hA);
+    store_tile(dA, gA, hA);
+  }
+  __syncthreads();
+  for (int t = t_beg; t < t_end; ++t) {
+    if (t + 1 < t_end) load_tile(t + 1, dA, gA, hA);
+    compute_tile();
     __syncthreads();
     if (t + 1 < t_end) {
-      store_tile();
+      store_tile(dA, gA, hA);
       __syncthreads();
     }
   }
+#else
+  // two tiles in flight (register sets A/B): a tile's global loads have two tile
+  // computations to land instead of one.  Invariant at the loop top: LDS holds
+  // tile t, set A holds (loads of) tile t+1
+  u32x4 dB[D_IT], gB[GD], hB[H_IT];
+  if (t_beg < t_end) {
+    load_tile(t_beg, dA, gA, hA);
+    store_tile(dA, gA, hA);
+  }
+  if (t_beg + 1 < t_end) load_tile(t_beg + 1, dA, gA, hA);
+  __syncthreads();
+  for (int t = t_beg; t < t_end; t += 2) {
+    if (t + 2 < t_end) load_tile(t + 2, dB, gB, hB);
+    compute_tile();
+    __syncthreads();
+    if (t + 1 >= t_end) break;
+    store_tile(dA, gA, hA);
+    __syncthreads();
+    if (t + 3 < t_end) load_tile(t + 3, dA, gA, hA);
+    compute_tile();
+    __syncthreads();
+    if (t + 2 < t_end) {
+      store_tile(dB, gB, hB);
+      __syncthreads();
+    }
+  }
+#endif
 
   if constexpr (GATE) {
     if (do_part) {
@@ -541,9 +576,23 @@ Plan plan(const rdn_wgrad_desc* d) {
 #ifndef RDN_NO_WROWS
   if (d->dtype == RDN_BF16) {
     // rows kernel: the widest channel group whose accumulators fit (BM x 9 CK per block)
+    // accumulator budget BM x CK (RDN_WROWS_MAXACC): <= 2560 keeps 2 blocks per CU,
+    // up to 4096 runs one block per CU with the wider channel group
+    static const int maxacc = [] {
+      const char* e = getenv("RDN_WROWS_MAXACC");
+      const int v = e ? atoi(e) : 2560;
+      return v < 2560 ? 2560 : v > 4096 ? 4096 : v;
+    }();
+    // RDN_WROWS_BM=128: 128 output channels per block for mdim >= 128 (dY tile read
+    // once per column group for twice the channels)
+    static const bool bm128 = [] {
+      const char* e = getenv("RDN_WROWS_BM");
+      return e && atoi(e) == 128;
+    }();
+    const int bm = bm128 && d->mdim >= 128 && maxacc >= 4096 ? 128 : p.bm;
     static const int cands[] = {96, 80, 64, 48, 32, 16, 8};
     for (int c : cands)
-      if (d->ndim % c == 0 && c * p.bm <= 2560) { p.ck = c; p.rows = 1; break; }
+      if (d->ndim % c == 0 && c * bm <= maxacc) { p.ck = c; p.rows = 1; p.bm = bm; break; }
   }
 #endif
   p.mtiles = (d->mdim + p.bm - 1) / p.bm;
@@ -582,7 +631,7 @@ int launch_w(const rdn_wgrad_desc* d, const Plan& p, hipStream_t st) {
 
 template <int BM, int CK>
 int launch_rows(const rdn_wgrad_desc* d, const Plan& p, hipStream_t st) {
-  if constexpr (CK * BM > 2560) {
+  if constexpr (CK * BM > 4096) {
     rdn_set_error("rdn_conv_wgrad(conv3): rows kernel BM=%d CK=%d", BM, CK);
     return RDN_E_SHAPE;
   } else {
@@ -634,6 +683,7 @@ int rdn_wgrad3_launch(const rdn_wgrad_desc* d, hipStream_t st) {
   if (p.rows) {
     if (p.bm == 16) return launch_rows_ck<16>(d, p, st);
     if (p.bm == 32) return launch_rows_ck<32>(d, p, st);
+    if (p.bm == 128) return launch_rows_ck<128>(d, p, st);
     return launch_rows_ck<64>(d, p, st);
   }
   if (d->dtype == RDN_BF16) {
