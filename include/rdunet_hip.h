@@ -89,6 +89,15 @@ typedef struct rdn_conv_desc {
      consumes dYpre computed on the fly from dY and the saved PReLU input
      (aten _prelu_kernel_backward fused into the input-gradient conv) */
   const void* gate; int64_t gate_ps; const float* gate_alpha;
+  /* channel-blocked ("planar") operands.  With *_pl == 0 an operand is plain NHWC:
+     channel c of pixel p sits at p*ps + c.  With *_pl > 0 its channels come in
+     blocks of ps, each block one contiguous [pixels][ps] plane, planes *_pl
+     elements apart: channel c of pixel p sits at (c/ps)*pl + p*ps + c%ps.  A conv
+     that reads or writes a channel slice of such a buffer then touches only the
+     planes of that slice (the dense-block buffers of Unet_model.py:81-89 are laid
+     out this way so conv_0..conv_2 do not drag the whole pixel row through HBM).
+     Channel offsets (x_c0, ...) count across planes; ps % (16 B / elem) == 0. */
+  int64_t x_pl, out_pl, pre_pl, res_pl, gate_pl;
 } rdn_conv_desc;
 
 /* Implicit-GEMM convolution (MFMA) with the fused epilogue above. */
@@ -111,6 +120,7 @@ typedef struct rdn_wgrad_desc {
      partials part[split][0][m] = sum_{gate<=0} gate*A, part[split][1][m] = sum
      gated A (dalpha / conv-bias gradients, summed by rdn_wgrad_reduce) */
   const void* a_gate; int64_t a_gate_ps; const float* a_gate_alpha; float* part;
+  int64_t a_pl, b_pl, a_gate_pl;   /* channel-blocked operands, as in rdn_conv_desc */
 } rdn_wgrad_desc;
 
 /* dW[m][tap][nd] partials = sum over pixels p of A[p][m] * B[gather(p,tap)][nd] */
@@ -135,9 +145,10 @@ int rdn_wgrad_reduce(const float* ws, int32_t splits, int32_t mdim, int32_t ndim
 /* PReLU backward (+ conv bias gradient) over a pixel grid of `pixels` pixels:
    dyp[p, c] = dy[p, c] * (pre[p, c] > 0 ? 1 : alpha[c])   (c < C; 0 for C <= c < cpad)
    dalpha[c] += sum_{pre<=0} pre*dy ; dbias[c] += sum dyp.
-   dy is NHWC (dy_ps, dy_c0) or, when dy_nchw != NULL, fp32 NCHW of the (n,h,w) grid. */
+   dy is NHWC (dy_ps, dy_c0, channel-blocked when dy_pl > 0) or, when dy_nchw != NULL, fp32
+   NCHW of the (n,h,w) grid. */
 int rdn_prelu_bwd(int32_t dtype, int64_t pixels, int32_t n, int32_t h, int32_t w, int32_t C, int32_t cpad,
-                  const void* dy, int64_t dy_ps, int32_t dy_c0, const float* dy_nchw,
+                  const void* dy, int64_t dy_ps, int32_t dy_c0, int64_t dy_pl, const float* dy_nchw,
                   const void* pre, int64_t pre_ps, const float* alpha,
                   void* dyp, float* dalpha, float* dbias, float* ws, void* stream);
 /* per-block channel partials (deterministic, no atomics): bytes of `ws` needed */
@@ -210,10 +221,10 @@ int rdn_adam_step(float* p, const float* g, float* m, float* v, int64_t count,
 int rdn_sampling_combine(float* x, const float* f1, const float* f2, const float* y, int64_t count,
                          float c1, float a, float c2, float ap, void* stream);
 
-/* dense layout converters (fp32 NCHW <-> NHWC slice of `dtype`) */
+/* dense layout converters (fp32 NCHW <-> NHWC slice of `dtype`, channel-blocked when *_pl > 0) */
 int rdn_nchw_to_nhwc(int32_t dtype, const float* src, int32_t n, int32_t c, int32_t h, int32_t w,
-                     void* dst, int64_t dst_ps, int32_t dst_c0, void* stream);
-int rdn_nhwc_to_nchw(int32_t dtype, const void* src, int64_t src_ps, int32_t src_c0,
+                     void* dst, int64_t dst_ps, int32_t dst_c0, int64_t dst_pl, int32_t accumulate, void* stream);
+int rdn_nhwc_to_nchw(int32_t dtype, const void* src, int64_t src_ps, int32_t src_c0, int64_t src_pl,
                      int32_t n, int32_t c, int32_t h, int32_t w, float* dst, int32_t accumulate, void* stream);
 
 /* fill a [pixels][cols] NHWC slice with zeros */

@@ -269,7 +269,7 @@ def test_prelu_bwd(dt, C_, cpad, nchw):
     da = torch.full((C_,), 0.5, device="cuda")   # accumulates into existing gradients
     db = torch.full((C_,), -0.25, device="cuda")
     ws = torch.zeros(H.lib().rdn_prelu_bwd_workspace_size(H.dtype_code(dt), P, C_, cpad) // 4, device="cuda")
-    H.check(H.lib().rdn_prelu_bwd(H.dtype_code(dt), P, N, Hh, Ww, C_, cpad, *dy_args, pre.data_ptr(), cpad,
+    H.check(H.lib().rdn_prelu_bwd(H.dtype_code(dt), P, N, Hh, Ww, C_, cpad, *dy_args[:3], 0, dy_args[3], pre.data_ptr(), cpad,
                                   a.data_ptr(), dyp.data_ptr(), da.data_ptr(), db.data_ptr(), ws.data_ptr(),
                                   H.stream_ptr()))
     torch.cuda.synchronize()
@@ -354,7 +354,7 @@ def test_fused_prelu_gate_matches_separate_pass(dt):
     dyp = torch.zeros(P, cout, dtype=dt, device="cuda")
     da1, db1 = torch.zeros(cout, device="cuda"), torch.zeros(cout, device="cuda")
     pws = torch.zeros(lib.rdn_prelu_bwd_workspace_size(code, P, cout, cout) // 4 + 4096, device="cuda")
-    H.check(lib.rdn_prelu_bwd(code, P, N, Hh, Ww, cout, cout, dyb.data_ptr(), Cd, 48, None, pre.data_ptr(), cout,
+    H.check(lib.rdn_prelu_bwd(code, P, N, Hh, Ww, cout, cout, dyb.data_ptr(), Cd, 48, 0, None, pre.data_ptr(), cout,
                               a.data_ptr(), dyp.data_ptr(), da1.data_ptr(), db1.data_ptr(), pws.data_ptr(), st))
 
     def dgrad(xp, xps, xc0, gate):
@@ -396,7 +396,7 @@ def test_fused_prelu_gate_matches_separate_pass(dt):
     # unfused path as the engine runs it: rdn_prelu_bwd leaves its partials, the
     # layer's rdn_wgrad_reduce sums them (part_splits = rdn_prelu_bwd_blocks)
     pws2 = torch.zeros_like(pws)
-    H.check(lib.rdn_prelu_bwd(code, P, N, Hh, Ww, cout, cout, dyb.data_ptr(), Cd, 48, None, pre.data_ptr(), cout,
+    H.check(lib.rdn_prelu_bwd(code, P, N, Hh, Ww, cout, cout, dyb.data_ptr(), Cd, 48, 0, None, pre.data_ptr(), cout,
                               a.data_ptr(), dyp.data_ptr(), None, None, pws2.data_ptr(), st))
     nb = lib.rdn_prelu_bwd_blocks(code, P, cout)
     da3, db3 = torch.zeros(cout, device="cuda"), torch.zeros(cout, device="cuda")

@@ -37,6 +37,7 @@ class ConvDesc(C.Structure):
         ("out_nchw", _vp), ("res_nchw", _vp),
         ("bm", _i32), ("bn", _i32),
         ("gate", _vp), ("gate_ps", _i64), ("gate_alpha", _vp),
+        ("x_pl", _i64), ("out_pl", _i64), ("pre_pl", _i64), ("res_pl", _i64), ("gate_pl", _i64),
     ]
 
 
@@ -47,6 +48,7 @@ class WgradDesc(C.Structure):
         ("b", _vp), ("b_ps", _i64), ("b_c0", _i32), ("ndim", _i32),
         ("ws", _vp), ("splits", _i32),
         ("a_gate", _vp), ("a_gate_ps", _i64), ("a_gate_alpha", _vp), ("part", _vp),
+        ("a_pl", _i64), ("b_pl", _i64), ("a_gate_pl", _i64),
     ]
 
 
@@ -71,7 +73,7 @@ SIGNATURES = {
     "rdn_wgrad_workspace_size": (_i64, [C.POINTER(WgradDesc)]),
     "rdn_wgrad_reduce": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _vp, _i32, _vp, _i32, _vp, _vp, _vp]),
     "rdn_prelu_bwd_blocks": (_i32, [_i32, _i64, _i32]),
-    "rdn_prelu_bwd": (_i32, [_i32, _i64, _i32, _i32, _i32, _i32, _i32, _vp, _i64, _i32, _vp, _vp, _i64, _vp,
+    "rdn_prelu_bwd": (_i32, [_i32, _i64, _i32, _i32, _i32, _i32, _i32, _vp, _i64, _i32, _i64, _vp, _vp, _i64, _vp,
                              _vp, _vp, _vp, _vp, _vp]),
     "rdn_prelu_bwd_workspace_size": (_i64, [_i32, _i64, _i32, _i32]),
     "rdn_interp": (_i32, [_vp, _vp, _vp, _i32, _i64, _vp, _vp]),
@@ -88,8 +90,8 @@ SIGNATURES = {
     "rdn_clip_scale": (_i32, [_vp, _i64, _vp, _vp]),
     "rdn_adam_step": (_i32, [_vp, _vp, _vp, _vp, _i64, _f32, _f32, _f32, _f32, _f32, _i32, _f32, _f32, _f32, _vp]),
     "rdn_sampling_combine": (_i32, [_vp, _vp, _vp, _vp, _i64, _f32, _f32, _f32, _f32, _vp]),
-    "rdn_nchw_to_nhwc": (_i32, [_i32, _vp, _i32, _i32, _i32, _i32, _vp, _i64, _i32, _vp]),
-    "rdn_nhwc_to_nchw": (_i32, [_i32, _vp, _i64, _i32, _i32, _i32, _i32, _i32, _vp, _i32, _vp]),
+    "rdn_nchw_to_nhwc": (_i32, [_i32, _vp, _i32, _i32, _i32, _i32, _vp, _i64, _i32, _i64, _i32, _vp]),
+    "rdn_nhwc_to_nchw": (_i32, [_i32, _vp, _i64, _i32, _i64, _i32, _i32, _i32, _i32, _vp, _i32, _vp]),
     "rdn_zero_slice": (_i32, [_i32, _vp, _i64, _i64, _i32, _i32, _vp]),
     "rdn_synth_batch": (_i32, [_vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "rdn_image_metrics_workspace_size": (_i64, [_i32, _i32, _i32, _i32]),

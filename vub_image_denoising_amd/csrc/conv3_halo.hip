@@ -84,9 +84,9 @@ __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_
   // ---- halo units of this thread (tile fixed for the block): element offset
   // from the halo origin, LDS offset, in-image flag; chunk c adds c * CK
   const int64_t hpix0 = ((int64_t)nimg * H + (y0 - 1)) * W + (x0 - 1);
-  const T* const xb = (const T*)d.x + hpix0 * d.x_ps + d.x_c0;
+  const T* const xb = (const T*)d.x + hpix0 * d.x_ps;
   const T* const gb = GATE ? (const T*)d.gate + hpix0 * d.gate_ps : nullptr;
-  int hrel[H_IT], grel[GATE ? H_IT : 1], hlds[H_IT];
+  int hrel[H_IT], grel[GATE ? H_IT : 1], hlds[H_IT], hcu[H_IT];
   bool hok[H_IT];
 #pragma unroll
   for (int it = 0; it < H_IT; ++it) {
@@ -94,8 +94,9 @@ __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_
     const int hp = u / HU, cu = u - hp * HU;
     const int hy = hp / (TW + 2), hx = hp - hy * (TW + 2);
     hok[it] = u < H_UNITS && (unsigned)(y0 - 1 + hy) < (unsigned)H && (unsigned)(x0 - 1 + hx) < (unsigned)W;
-    hrel[it] = (hy * W + hx) * (int)d.x_ps + cu * VEC;
-    if constexpr (GATE) grel[it] = (hy * W + hx) * (int)d.gate_ps + cu * VEC;
+    hrel[it] = (hy * W + hx) * (int)d.x_ps;
+    if constexpr (GATE) grel[it] = (hy * W + hx) * (int)d.gate_ps;
+    hcu[it] = cu * VEC;
     hlds[it] = u < H_UNITS ? hp * HROW + cu * 16 : -1;
   }
   u32x4 hreg[H_IT];
@@ -110,8 +111,9 @@ __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_
     for (int it = 0; it < H_IT; ++it) {
       u32x4 v = {0u, 0u, 0u, 0u}, gv = {0u, 0u, 0u, 0u};
       if (hok[it]) {
-        v = *(const u32x4*)(xb + hrel[it] + c * CK);
-        if constexpr (GATE) gv = *(const u32x4*)(gb + grel[it] + c * CK);
+        // channel offset of this unit in chunk c (channel-blocked operands: rdn_coff)
+        v = *(const u32x4*)(xb + hrel[it] + rdn_coff(d.x_c0 + c * CK + hcu[it], d.x_ps, d.x_pl));
+        if constexpr (GATE) gv = *(const u32x4*)(gb + grel[it] + rdn_coff(c * CK + hcu[it], d.gate_ps, d.gate_pl));
       }
       hreg[it] = v;
       if constexpr (GATE) greg[it] = gv;
@@ -252,6 +254,7 @@ __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_
   }
   const int64_t opix0 = ((int64_t)nimg * H + y0) * W + x0;
   float ebias[VEC], ealpha[VEC];
+  int64_t cf_pre = 0, cf_out = 0, cf_res = 0;
   if constexpr (COLFIX) {
     const int c = n0 + (tid % UPR) * VEC;
 #pragma unroll
@@ -259,6 +262,9 @@ __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_
       ebias[q] = ((flags & RDN_EPI_BIAS) && c + q < d.ncols) ? d.bias[c + q] : 0.f;
       ealpha[q] = ((flags & RDN_EPI_PRELU) && c + q < d.ncols) ? d.alpha[c + q] : 0.f;
     }
+    cf_pre = rdn_coff(c, d.pre_ps, d.pre_pl);
+    cf_out = rdn_coff(d.out_c0 + c, d.out_ps, d.out_pl);
+    cf_res = rdn_coff(d.res_c0 + c, d.res_ps, d.res_pl);
   }
 #pragma unroll
   for (int it = 0; it < E_IT; ++it) {
@@ -278,7 +284,8 @@ __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_
 #pragma unroll
       for (int q = 0; q < VEC; ++q) v[q] += COLFIX ? ebias[q] : d.bias[c + q];
     }
-    if (flags & RDN_EPI_STORE_PRE) *(u32x4*)((T*)d.pre + opix * d.pre_ps + c) = Unit16<T>::pack(v);
+    if (flags & RDN_EPI_STORE_PRE)
+      *(u32x4*)((T*)d.pre + opix * d.pre_ps + (COLFIX ? cf_pre : rdn_coff(c, d.pre_ps, d.pre_pl))) = Unit16<T>::pack(v);
     if (flags & RDN_EPI_PRELU) {
 #pragma unroll
       for (int q = 0; q < VEC; ++q) {
@@ -286,10 +293,11 @@ __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_
         v[q] = v[q] > 0.f ? v[q] : a * v[q];
       }
     }
-    T* const op = (T*)d.out + opix * d.out_ps + d.out_c0 + c;
+    T* const op = (T*)d.out + opix * d.out_ps + (COLFIX ? cf_out : rdn_coff(d.out_c0 + c, d.out_ps, d.out_pl));
     float rv[VEC];
     if ((flags & RDN_EPI_RESID) && c < d.res_climit) {
-      Unit16<T>::unpack(*(const u32x4*)((const T*)d.res + opix * d.res_ps + d.res_c0 + c), rv);
+      Unit16<T>::unpack(*(const u32x4*)((const T*)d.res + opix * d.res_ps +
+                                        (COLFIX ? cf_res : rdn_coff(d.res_c0 + c, d.res_ps, d.res_pl))), rv);
 #pragma unroll
       for (int q = 0; q < VEC; ++q) v[q] += rv[q];
     }

@@ -34,7 +34,7 @@ __device__ __forceinline__ void finish_unit(const rdn_conv_desc& d, float* v, in
     for (int q = 0; q < VEC; ++q) v[q] += (c + q < d.ncols) ? d.bias[c + q] : 0.f;
   }
   if (flags & RDN_EPI_STORE_PRE) {
-    T* pp = (T*)d.pre + opix * d.pre_ps + c;
+    T* pp = (T*)d.pre + opix * d.pre_ps + rdn_coff(c, d.pre_ps, d.pre_pl);
     if (full) *(u32x4*)pp = Unit16<T>::pack(v);
     else {
 #pragma unroll
@@ -62,7 +62,7 @@ __device__ __forceinline__ void finish_unit(const rdn_conv_desc& d, float* v, in
     return;
   }
   if (flags & RDN_EPI_RESID) {
-    const T* rp = (const T*)d.res + opix * d.res_ps + d.res_c0 + c;
+    const T* rp = (const T*)d.res + opix * d.res_ps + rdn_coff(d.res_c0 + c, d.res_ps, d.res_pl);
     if (full && c + VEC <= d.res_climit) {
       float rv[VEC];
       Unit16<T>::unpack(pf_kind == PF_RES ? pf : *(const u32x4*)rp, rv);
@@ -74,7 +74,7 @@ __device__ __forceinline__ void finish_unit(const rdn_conv_desc& d, float* v, in
         if (c + q < d.res_climit && c + q < d.ncols) v[q] += to_f32(rp[q]);
     }
   }
-  T* op = (T*)d.out + opix * d.out_ps + d.out_c0 + c;
+  T* op = (T*)d.out + opix * d.out_ps + rdn_coff(d.out_c0 + c, d.out_ps, d.out_pl);
   if (full) {
     if (flags & RDN_EPI_ACCUM) {
       float ov[VEC];

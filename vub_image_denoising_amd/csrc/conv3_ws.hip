@@ -93,6 +93,7 @@ __global__ __launch_bounds__(NT, 2) void conv3_ws_kernel(rdn_conv_desc d, int ti
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int H = d.h, W = d.w;
+  const int flags = d.flags;
 
   // this block's tiles: XCD share [t_lo, t_hi), strided by the XCD's block count
   const int per = gridDim.x >> 3;
@@ -116,14 +117,21 @@ __global__ __launch_bounds__(NT, 2) void conv3_ws_kernel(rdn_conv_desc d, int ti
 
   // ---- tile-invariant per-thread geometry, computed once: every address below is
   // a per-tile uniform base plus one of these offsets (no per-tile index math)
+  // Unit order of the halo loads: pixel-major (u -> pixel, 16-B unit) for plain
+  // operands; plane-major for channel-blocked ones (u -> plane, pixel, unit in the
+  // plane row), so the lanes of one load instruction walk consecutive pixels of ONE
+  // plane instead of scattering over every plane a pixel spans.  The LDS image is
+  // the same either way.  GATE keeps one channel unit per thread (galpha).
+  const int hupp = (!GATE && d.x_pl && d.x_c0 % d.x_ps == 0 && HU % (d.x_ps / VEC) == 0) ? (int)(d.x_ps / VEC) : HU;
   int hrel[H_IT], grel[GATE ? H_IT : 1], hlds[H_IT];
 #pragma unroll
   for (int it = 0; it < H_IT; ++it) {
     const int u = tid + it * NT;
-    const int hp = u / HU, cu = u - hp * HU;
+    const int pln = u / (HW_ * hupp), rem = u - pln * (HW_ * hupp);
+    const int hp = u < H_UNITS ? rem / hupp : HW_ - 1, cu = u < H_UNITS ? pln * hupp + rem % hupp : 0;
     const int hy = hp / (TW + 2), hx = hp - hy * (TW + 2);
-    hrel[it] = (hy * W + hx) * d.x_ps + cu * VEC;
-    if constexpr (GATE) grel[it] = (hy * W + hx) * d.gate_ps + cu * VEC;
+    hrel[it] = (hy * W + hx) * (int)d.x_ps + rdn_coff32(d.x_c0 + cu * VEC, (int)d.x_ps, (int)d.x_pl);
+    if constexpr (GATE) grel[it] = (hy * W + hx) * (int)d.gate_ps + rdn_coff32(cu * VEC, (int)d.gate_ps, (int)d.gate_pl);
     hlds[it] = hp * HROW + cu * 16;
   }
   // A-operand LDS offsets per k-step (lane group g covers k = 32 j + 8 g .. +7):
@@ -155,13 +163,26 @@ __global__ __launch_bounds__(NT, 2) void conv3_ws_kernel(rdn_conv_desc d, int ti
   }
   if constexpr (COLFIX) ecol[0] = (tid % UPR) * VEC;
   auto col_of = [&](int it) { return COLFIX ? ecol[0] : ecol[it]; };
+  // channel offsets of an output unit in the pre / out / residual operands
+  // (channel-blocked layouts: rdn_coff); fixed per thread when COLFIX
+  // (32-bit: the host checks channel-blocked offsets stay below 2^31)
+  int cf_pre = 0, cf_out = 0, cf_res = 0;
+  if constexpr (COLFIX) {
+    cf_pre = rdn_coff32(ecol[0], (int)d.pre_ps, (int)d.pre_pl);
+    cf_out = rdn_coff32(d.out_c0 + ecol[0], (int)d.out_ps, (int)d.out_pl);
+    cf_res = rdn_coff32(d.res_c0 + ecol[0], (int)d.res_ps, (int)d.res_pl);
+  }
+  auto off_pre = [&](int c) { return COLFIX ? cf_pre : rdn_coff32(c, (int)d.pre_ps, (int)d.pre_pl); };
+  auto off_out = [&](int c) { return COLFIX ? cf_out : rdn_coff32(d.out_c0 + c, (int)d.out_ps, (int)d.out_pl); };
+  auto off_res = [&](int c) { return COLFIX ? cf_res : rdn_coff32(d.res_c0 + c, (int)d.res_ps, (int)d.res_pl); };
 
-  const int flags = d.flags;
   // fast epilogue: whole 16-B NHWC units, no NCHW output
   const bool fast_epi = (d.ncols % VEC) == 0 && !(flags & RDN_EPI_OUT_NCHW) &&
                         (!(flags & RDN_EPI_RESID) || (d.res_climit % VEC == 0 && d.res_ps % VEC == 0 &&
                                                       d.res_c0 % VEC == 0)) &&
                         d.out_ps % VEC == 0 && d.out_c0 % VEC == 0 && d.pre_ps % VEC == 0;
+  // bias / PReLU slope of a thread's fixed column, in registers (colfix); other
+  // orders read them per unit (L1-resident, a few hundred bytes)
   float ebias[COLFIX ? VEC : 1], ealpha[COLFIX ? VEC : 1];
   if constexpr (COLFIX) {
 #pragma unroll
@@ -190,7 +211,7 @@ __global__ __launch_bounds__(NT, 2) void conv3_ws_kernel(rdn_conv_desc d, int ti
   };
   auto load_halo = [&](int oy, int ox, int on) {
     const int64_t hpix0 = ((int64_t)on * H + (oy - 1)) * W + (ox - 1);   // halo pixel (0, 0)
-    const bf16* const xb = X + hpix0 * d.x_ps + d.x_c0;
+    const bf16* const xb = X + hpix0 * d.x_ps;
     const bf16* const gb = GATE ? G + hpix0 * d.gate_ps : nullptr;
     const bool interior = oy >= 1 && oy + TH + 1 <= H && ox >= 1 && ox + TW + 1 <= W;
 #pragma unroll
@@ -198,7 +219,7 @@ __global__ __launch_bounds__(NT, 2) void conv3_ws_kernel(rdn_conv_desc d, int ti
       const int u = tid + it * NT;
       bool ok = (it + 1 < H_IT) || u < H_UNITS;
       if (!interior) {
-        const int hp = u / HU;
+        const int hp = hlds[it] / HROW;   // this unit's halo pixel (pixel- or plane-major order)
         const int hy = hp / (TW + 2), hx = hp - hy * (TW + 2);
         ok = ok && (unsigned)(oy - 1 + hy) < (unsigned)H && (unsigned)(ox - 1 + hx) < (unsigned)W;
       }
@@ -238,14 +259,14 @@ __global__ __launch_bounds__(NT, 2) void conv3_ws_kernel(rdn_conv_desc d, int ti
     if constexpr (!PF) return;
     if (!(pf_res || pf_acc) || oy + TH > H || ox + TW > W) return;
     const int64_t opix0 = ((int64_t)on * H + oy) * W + ox;
-    const bf16* const base = pf_res ? (const bf16*)d.res + opix0 * d.res_ps + d.res_c0
-                                    : (const bf16*)d.out + opix0 * d.out_ps + d.out_c0;
+    const bf16* const base = pf_res ? (const bf16*)d.res + opix0 * d.res_ps : (const bf16*)d.out + opix0 * d.out_ps;
     const int ps = pf_res ? d.res_ps : d.out_ps;
 #pragma unroll
     for (int it = 0; it < E_IT; ++it) {
       if (it + 1 == E_IT && tid + it * NT >= EU) continue;
       const int c = col_of(it);
-      if (c < (pf_res ? d.res_climit : d.ncols)) eop[it] = *(const u32x4*)(base + erel[it] * ps + c);
+      if (c < (pf_res ? d.res_climit : d.ncols))
+        eop[it] = *(const u32x4*)(base + erel[it] * ps + (pf_res ? off_res(c) : off_out(c)));
     }
   };
 
@@ -328,7 +349,7 @@ __global__ __launch_bounds__(NT, 2) void conv3_ws_kernel(rdn_conv_desc d, int ti
 #pragma unroll
             for (int q = 0; q < VEC; ++q) v[q] += COLFIX ? ebias[q] : d.bias[c + q];
           }
-          if (flags & RDN_EPI_STORE_PRE) *(u32x4*)((bf16*)d.pre + opix * d.pre_ps + c) = Unit16<bf16>::pack(v);
+          if (flags & RDN_EPI_STORE_PRE) *(u32x4*)((bf16*)d.pre + opix * d.pre_ps + off_pre(c)) = Unit16<bf16>::pack(v);
           if (flags & RDN_EPI_PRELU) {
 #pragma unroll
             for (int q = 0; q < VEC; ++q) {
@@ -336,12 +357,12 @@ __global__ __launch_bounds__(NT, 2) void conv3_ws_kernel(rdn_conv_desc d, int ti
               v[q] = v[q] > 0.f ? v[q] : a * v[q];
             }
           }
-          bf16* const op = (bf16*)d.out + opix * d.out_ps + d.out_c0 + c;
+          bf16* const op = (bf16*)d.out + opix * d.out_ps + off_out(c);
           if (flags & (RDN_EPI_RESID | RDN_EPI_ACCUM)) {
             float rv[VEC];
             if ((flags & RDN_EPI_RESID) && c < d.res_climit) {
               Unit16<bf16>::unpack(pf_res ? eop[PF ? it : 0]
-                                          : *(const u32x4*)((const bf16*)d.res + opix * d.res_ps + d.res_c0 + c),
+                                          : *(const u32x4*)((const bf16*)d.res + opix * d.res_ps + off_res(c)),
                                    rv);
 #pragma unroll
               for (int q = 0; q < VEC; ++q) v[q] += rv[q];

@@ -71,10 +71,11 @@ __global__ __launch_bounds__(NT) void conv_gemm_kernel(rdn_conv_desc d, FastDiv 
     const uint32_t x = rem - y * (uint32_t)d.w;
     a_y[r] = (int)y;
     a_x[r] = (int)x;
+    // pixel part only; the channel part (rdn_coff) is added per K stage
     if (GATHER == RDN_G_S2)
-      a_base[r] = (((int64_t)nimg * d.hin + 2 * y) * d.win + 2 * x) * d.x_ps + d.x_c0;
+      a_base[r] = (((int64_t)nimg * d.hin + 2 * y) * d.win + 2 * x) * d.x_ps;
     else
-      a_base[r] = (((int64_t)nimg * d.hin + y) * d.win + x) * d.x_ps + d.x_c0;
+      a_base[r] = (((int64_t)nimg * d.hin + y) * d.win + x) * d.x_ps;
   }
 
   const int cin = d.cin;
@@ -85,6 +86,7 @@ __global__ __launch_bounds__(NT) void conv_gemm_kernel(rdn_conv_desc d, FastDiv 
   u32x4 ra[A_IT], rb[B_IT];
 
   auto load_stage = [&](int s) {
+    const int64_t cf = rdn_coff(d.x_c0 + ci, d.x_ps, d.x_pl);   // this thread's channel unit
 #pragma unroll
     for (int r = 0; r < A_IT; ++r) {
       u32x4 v = {0u, 0u, 0u, 0u};
@@ -95,11 +97,11 @@ __global__ __launch_bounds__(NT) void conv_gemm_kernel(rdn_conv_desc d, FastDiv 
           const int dy = tap / 3 - 1, dx = tap % 3 - 1;
           const int ys = a_y[r] + dy, xs = a_x[r] + dx;
           ok = (ys >= 0) && (ys < d.hin) && (xs >= 0) && (xs < d.win);
-          off = a_base[r] + ((int64_t)dy * d.win + dx) * d.x_ps + ci;
+          off = a_base[r] + ((int64_t)dy * d.win + dx) * d.x_ps + cf;
         } else if (GATHER == RDN_G_S2) {
-          off = a_base[r] + ((int64_t)(tap >> 1) * d.win + (tap & 1)) * d.x_ps + ci;
+          off = a_base[r] + ((int64_t)(tap >> 1) * d.win + (tap & 1)) * d.x_ps + cf;
         } else {
-          off = a_base[r] + ci;
+          off = a_base[r] + cf;
         }
         if (ok) v = *(const u32x4*)(X + off);
       }
@@ -212,6 +214,8 @@ __global__ __launch_bounds__(NT) void conv_gemm_kernel(rdn_conv_desc d, FastDiv 
       ea[q] = (flags & RDN_EPI_PRELU) ? d.alpha[c + q] : 0.f;
     }
     const bool resid = (flags & RDN_EPI_RESID) && c < d.res_climit;
+    const int64_t cf_pre = rdn_coff(c, d.pre_ps, d.pre_pl), cf_out = rdn_coff(d.out_c0 + c, d.out_ps, d.out_pl);
+    const int64_t cf_res = rdn_coff(d.res_c0 + c, d.res_ps, d.res_pl);
 #pragma unroll 2
     for (int r = tid / UPR; r < BM; r += RPI) {
       const int64_t m = m0 + r;
@@ -235,16 +239,16 @@ __global__ __launch_bounds__(NT) void conv_gemm_kernel(rdn_conv_desc d, FastDiv 
 #pragma unroll
         for (int q = 0; q < VEC; ++q) v[q] += eb[q];
       }
-      if (flags & RDN_EPI_STORE_PRE) *(u32x4*)((T*)d.pre + opix * d.pre_ps + c) = Unit16<T>::pack(v);
+      if (flags & RDN_EPI_STORE_PRE) *(u32x4*)((T*)d.pre + opix * d.pre_ps + cf_pre) = Unit16<T>::pack(v);
       if (flags & RDN_EPI_PRELU) {
 #pragma unroll
         for (int q = 0; q < VEC; ++q) v[q] = v[q] > 0.f ? v[q] : ea[q] * v[q];
       }
-      T* const op = (T*)d.out + opix * d.out_ps + d.out_c0 + c;
+      T* const op = (T*)d.out + opix * d.out_ps + cf_out;
       if (resid || (flags & RDN_EPI_ACCUM)) {
         float rv[VEC];
         if (resid) {
-          Unit16<T>::unpack(*(const u32x4*)((const T*)d.res + opix * d.res_ps + d.res_c0 + c), rv);
+          Unit16<T>::unpack(*(const u32x4*)((const T*)d.res + opix * d.res_ps + cf_res), rv);
 #pragma unroll
           for (int q = 0; q < VEC; ++q) v[q] += rv[q];
         }
@@ -332,6 +336,11 @@ extern "C" int rdn_conv_fwd(const rdn_conv_desc* d, void* stream) {
   if (d->cin % 8 || d->x_ps % vec || d->x_c0 % vec || d->kp % 64 || ((uintptr_t)d->x & 15) || ((uintptr_t)d->wp & 15)) {
     rdn_set_error("rdn_conv_fwd: alignment (cin=%d x_ps=%lld x_c0=%d kp=%d) must keep 16-byte units", d->cin,
                   (long long)d->x_ps, d->x_c0, d->kp);
+    return RDN_E_SHAPE;
+  }
+  if ((d->x_pl && (d->x_pl < (int64_t)d->n * d->hin * d->win * d->x_ps || rdn_coff(d->x_c0 + d->cin - 1, d->x_ps, d->x_pl) >= (1ll << 31))) ||
+      (d->out_pl && d->out_ps % vec) || (d->res_pl && d->res_ps % vec) || (d->gate_pl && d->gate_ps % vec)) {
+    rdn_set_error("rdn_conv_fwd: channel-blocked operand needs ps %% %d == 0, planes >= pixels*ps apart, offsets < 2^31", vec);
     return RDN_E_SHAPE;
   }
   const int taps = d->gather == RDN_G_CONV3 ? 9 : d->gather == RDN_G_S2 ? 4 : 1;

@@ -59,6 +59,9 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(rdn_wgrad_desc d, FastDiv fd_
   const bool b_col_ok = bcol < ncol;
   const int btap = b_col_ok ? bcol / d.ndim : 0;
   const int bnd = bcol - btap * d.ndim;
+  // channel offsets (channel-blocked operands: rdn_coff), fixed per thread
+  const int64_t a_cf = rdn_coff(d.a_c0 + am, d.a_ps, d.a_pl);
+  const int64_t b_cf = rdn_coff(d.b_c0 + bnd, d.b_ps, d.b_pl);
   int bdy, bdx;
   if (GATHER == RDN_G_CONV3) { bdy = btap / 3 - 1; bdx = btap % 3 - 1; }
   else { bdy = btap >> 1; bdx = btap & 1; }
@@ -70,7 +73,7 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(rdn_wgrad_desc d, FastDiv fd_
       const int u = tid + r * NT;
       const int64_t p = pb + u / AG;
       u32x4 v = {0u, 0u, 0u, 0u};
-      if (u < A_UNITS && a_col_ok && p < pend) v = *(const u32x4*)(A + p * d.a_ps + d.a_c0 + am);
+      if (u < A_UNITS && a_col_ok && p < pend) v = *(const u32x4*)(A + p * d.a_ps + a_cf);
       ra[r] = v;
     }
 #pragma unroll
@@ -87,7 +90,7 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(rdn_wgrad_desc d, FastDiv fd_
         if (GATHER == RDN_G_CONV3) { ys = y + bdy; xs = x + bdx; }
         else { ys = 2 * y + bdy; xs = 2 * x + bdx; }
         if (ys >= 0 && ys < d.hin && xs >= 0 && xs < d.win)
-          v = *(const u32x4*)(B + (((int64_t)nimg * d.hin + ys) * d.win + xs) * d.b_ps + d.b_c0 + bnd);
+          v = *(const u32x4*)(B + (((int64_t)nimg * d.hin + ys) * d.win + xs) * d.b_ps + b_cf);
       }
       rb[r] = v;
     }
@@ -323,6 +326,11 @@ extern "C" int rdn_conv_wgrad(const rdn_wgrad_desc* d, void* stream) {
       ((uintptr_t)d->a & 15) || ((uintptr_t)d->b & 15)) {
     rdn_set_error("rdn_conv_wgrad: alignment (ndim=%d a_ps=%lld a_c0=%d b_ps=%lld b_c0=%d)", d->ndim,
                   (long long)d->a_ps, d->a_c0, (long long)d->b_ps, d->b_c0);
+    return RDN_E_SHAPE;
+  }
+  if ((d->a_pl && rdn_coff(d->a_c0 + d->mdim - 1, d->a_ps, d->a_pl) >= (1ll << 31)) ||
+      (d->b_pl && rdn_coff(d->b_c0 + d->ndim - 1, d->b_ps, d->b_pl) >= (1ll << 31))) {
+    rdn_set_error("rdn_conv_wgrad: channel-blocked operand offsets must stay below 2^31 elements");
     return RDN_E_SHAPE;
   }
   if (d->gather == RDN_G_S2 ? (d->hin != 2 * d->h || d->win != 2 * d->w) : (d->hin != d->h || d->win != d->w)) {

@@ -76,7 +76,7 @@ static int grid_for(int64_t n, int per_block, int cap = 8192) {
 template <typename T>
 __global__ __launch_bounds__(256) void prelu_bwd_kernel(int64_t pixels, int H, int W, int C, int cpad,
                                                         const T* __restrict__ dy, int64_t dy_ps, int dy_c0,
-                                                        const float* __restrict__ dy_nchw, const T* __restrict__ pre,
+                                                        int64_t dy_pl, const float* __restrict__ dy_nchw, const T* __restrict__ pre,
                                                         int64_t pre_ps, const float* __restrict__ alpha, T* __restrict__ dyp,
                                                         float* __restrict__ part) {
   constexpr int VEC = TypeInfo<T>::VEC;
@@ -94,6 +94,7 @@ __global__ __launch_bounds__(256) void prelu_bwd_kernel(int64_t pixels, int H, i
   }
   const int64_t stride = (int64_t)gridDim.x * ppb;
   int64_t p0 = (int64_t)blockIdx.x * ppb + pl;
+  const int64_t dy_cf = rdn_coff(dy_c0 + grp * VEC, dy_ps, dy_pl);   // channel offset of this thread's unit
 #ifndef RDN_NO_PRELU_UNROLL
   // NHWC fast path: 4 pixel iterations per trip with all 8 loads issued first
   // (unconditional, from a clamped valid pixel) -- the plain loop exposes one
@@ -105,7 +106,7 @@ __global__ __launch_bounds__(256) void prelu_bwd_kernel(int64_t pixels, int H, i
       for (int u = 0; u < 4; ++u) {
         const int64_t pu = p0 + u * stride;
         const int64_t pc = pu < pixels ? pu : p0;
-        gv[u] = *(const u32x4*)(dy + pc * dy_ps + dy_c0 + grp * VEC);
+        gv[u] = *(const u32x4*)(dy + pc * dy_ps + dy_cf);
         xv[u] = *(const u32x4*)(pre + pc * pre_ps + grp * VEC);
       }
 #pragma unroll
@@ -141,7 +142,7 @@ __global__ __launch_bounds__(256) void prelu_bwd_kernel(int64_t pixels, int H, i
           g[k] = c < C ? dy_nchw[(nimg * C + c) * hw + r] : 0.f;
         }
       } else {
-        const T* src = dy + p * dy_ps + dy_c0 + grp * VEC;
+        const T* src = dy + p * dy_ps + dy_cf;
         if (((dy_ps | dy_c0) % VEC) == 0) {
           Unit16<T>::unpack(*(const u32x4*)src, g);
         } else {
@@ -407,25 +408,27 @@ __global__ void sampling_combine_kernel(float* __restrict__ x, const float* __re
 
 template <typename T>
 __global__ void nchw_to_nhwc_kernel(const float* __restrict__ s, int N, int C, int H, int W, T* __restrict__ d,
-                                    int64_t ps, int c0) {
+                                    int64_t ps, int c0, int64_t pl, int acc) {
   const int64_t HW = (int64_t)H * W, total = (int64_t)N * C * HW;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t p = i / C;
     const int c = (int)(i - p * C);
     const int64_t n = p / HW, r = p - n * HW;
-    d[p * ps + c0 + c] = from_f32<T>(s[(n * C + c) * HW + r]);
+    T* const o = d + p * ps + rdn_coff(c0 + c, ps, pl);
+    const float v = s[(n * C + c) * HW + r];
+    *o = from_f32<T>(acc ? to_f32(*o) + v : v);
   }
 }
 
 template <typename T>
-__global__ void nhwc_to_nchw_kernel(const T* __restrict__ s, int64_t ps, int c0, int N, int C, int H, int W,
+__global__ void nhwc_to_nchw_kernel(const T* __restrict__ s, int64_t ps, int c0, int64_t pl, int N, int C, int H, int W,
                                     float* __restrict__ d, int acc) {
   const int64_t HW = (int64_t)H * W, total = (int64_t)N * C * HW;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t r = i % HW, nc = i / HW;
     const int c = (int)(nc % C);
     const int64_t n = nc / C;
-    const float v = to_f32(s[(n * HW + r) * ps + c0 + c]);
+    const float v = to_f32(s[(n * HW + r) * ps + rdn_coff(c0 + c, ps, pl)]);
     d[i] = acc ? d[i] + v : v;
   }
 }
@@ -460,7 +463,7 @@ extern "C" int64_t rdn_prelu_bwd_workspace_size(int32_t dtype, int64_t pixels, i
 }
 
 extern "C" int rdn_prelu_bwd(int32_t dtype, int64_t pixels, int32_t n, int32_t h, int32_t w, int32_t C, int32_t cpad,
-                             const void* dy, int64_t dy_ps, int32_t dy_c0, const float* dy_nchw, const void* pre,
+                             const void* dy, int64_t dy_ps, int32_t dy_c0, int64_t dy_pl, const float* dy_nchw, const void* pre,
                              int64_t pre_ps, const float* alpha, void* dyp, float* dalpha, float* dbias, float* ws,
                              void* stream) {
   const int vec = dtype == RDN_BF16 ? 8 : 4;
@@ -471,10 +474,10 @@ extern "C" int rdn_prelu_bwd(int32_t dtype, int64_t pixels, int32_t n, int32_t h
   }
   const int blocks = prelu_blocks(dtype, pixels, cpad);
   if (dtype == RDN_BF16)
-    prelu_bwd_kernel<bf16><<<blocks, 256, 0, RDN_STREAM>>>(pixels, h, w, C, cpad, (const bf16*)dy, dy_ps, dy_c0, dy_nchw,
+    prelu_bwd_kernel<bf16><<<blocks, 256, 0, RDN_STREAM>>>(pixels, h, w, C, cpad, (const bf16*)dy, dy_ps, dy_c0, dy_pl, dy_nchw,
                                                           (const bf16*)pre, pre_ps, alpha, (bf16*)dyp, ws);
   else
-    prelu_bwd_kernel<float><<<blocks, 256, 0, RDN_STREAM>>>(pixels, h, w, C, cpad, (const float*)dy, dy_ps, dy_c0, dy_nchw,
+    prelu_bwd_kernel<float><<<blocks, 256, 0, RDN_STREAM>>>(pixels, h, w, C, cpad, (const float*)dy, dy_ps, dy_c0, dy_pl, dy_nchw,
                                                            (const float*)pre, pre_ps, alpha, (float*)dyp, ws);
   if (dalpha || dbias) prelu_finalize_kernel<<<2 * C, 256, 0, RDN_STREAM>>>(ws, blocks, C, dalpha, dbias);
   return rdn_check_launch("rdn_prelu_bwd");
@@ -586,24 +589,28 @@ extern "C" int rdn_sampling_combine(float* x, const float* f1, const float* f2, 
 }
 
 extern "C" int rdn_nchw_to_nhwc(int32_t dtype, const float* src, int32_t n, int32_t c, int32_t h, int32_t w, void* dst,
-                                int64_t dst_ps, int32_t dst_c0, void* stream) {
-  if (!src || !dst) { rdn_set_error("rdn_nchw_to_nhwc: null"); return RDN_E_ARG; }
+                                int64_t dst_ps, int32_t dst_c0, int64_t dst_pl, int32_t accumulate, void* stream) {
+  if (!src || !dst || dst_ps <= 0) { rdn_set_error("rdn_nchw_to_nhwc: null / bad stride"); return RDN_E_ARG; }
   const int64_t total = (int64_t)n * c * h * w;
   if (dtype == RDN_BF16)
-    nchw_to_nhwc_kernel<bf16><<<grid_for(total, 256 * 4), 256, 0, RDN_STREAM>>>(src, n, c, h, w, (bf16*)dst, dst_ps, dst_c0);
+    nchw_to_nhwc_kernel<bf16><<<grid_for(total, 256 * 4), 256, 0, RDN_STREAM>>>(src, n, c, h, w, (bf16*)dst, dst_ps, dst_c0,
+                                                                              dst_pl, accumulate);
   else
-    nchw_to_nhwc_kernel<float><<<grid_for(total, 256 * 4), 256, 0, RDN_STREAM>>>(src, n, c, h, w, (float*)dst, dst_ps, dst_c0);
+    nchw_to_nhwc_kernel<float><<<grid_for(total, 256 * 4), 256, 0, RDN_STREAM>>>(src, n, c, h, w, (float*)dst, dst_ps, dst_c0,
+                                                                               dst_pl, accumulate);
   return rdn_check_launch("rdn_nchw_to_nhwc");
 }
 
-extern "C" int rdn_nhwc_to_nchw(int32_t dtype, const void* src, int64_t src_ps, int32_t src_c0, int32_t n, int32_t c,
-                                int32_t h, int32_t w, float* dst, int32_t accumulate, void* stream) {
-  if (!src || !dst) { rdn_set_error("rdn_nhwc_to_nchw: null"); return RDN_E_ARG; }
+extern "C" int rdn_nhwc_to_nchw(int32_t dtype, const void* src, int64_t src_ps, int32_t src_c0, int64_t src_pl, int32_t n,
+                                int32_t c, int32_t h, int32_t w, float* dst, int32_t accumulate, void* stream) {
+  if (!src || !dst || src_ps <= 0) { rdn_set_error("rdn_nhwc_to_nchw: null / bad stride"); return RDN_E_ARG; }
   const int64_t total = (int64_t)n * c * h * w;
   if (dtype == RDN_BF16)
-    nhwc_to_nchw_kernel<bf16><<<grid_for(total, 256 * 4), 256, 0, RDN_STREAM>>>((const bf16*)src, src_ps, src_c0, n, c, h, w, dst, accumulate);
+    nhwc_to_nchw_kernel<bf16><<<grid_for(total, 256 * 4), 256, 0, RDN_STREAM>>>((const bf16*)src, src_ps, src_c0, src_pl, n, c, h,
+                                                                              w, dst, accumulate);
   else
-    nhwc_to_nchw_kernel<float><<<grid_for(total, 256 * 4), 256, 0, RDN_STREAM>>>((const float*)src, src_ps, src_c0, n, c, h, w, dst, accumulate);
+    nhwc_to_nchw_kernel<float><<<grid_for(total, 256 * 4), 256, 0, RDN_STREAM>>>((const float*)src, src_ps, src_c0, src_pl, n, c,
+                                                                               h, w, dst, accumulate);
   return rdn_check_launch("rdn_nhwc_to_nchw");
 }
 

@@ -61,6 +61,17 @@ template <> struct Unit16<bf16> {
   }
 };
 
+// Element offset of channel c (counted across planes) within a pixel of an operand
+// with pixel stride ps and plane stride pl (include/rdunet_hip.h: pl == 0 is plain
+// NHWC, else channels come in [pixels][ps] planes).  A 16-byte unit never
+// straddles two planes (ps % VEC == 0), so offset(c + q) = offset(c) + q inside it.
+__host__ __device__ __forceinline__ int64_t rdn_coff(int c, int64_t ps, int64_t pl) {
+  return pl ? (int64_t)(c / (int)ps) * pl + (c % (int)ps) : (int64_t)c;
+}
+
+// 32-bit form for per-thread offsets the launchers have checked to stay below 2^31
+__device__ __forceinline__ int rdn_coff32(int c, int ps, int pl) { return pl ? (c / ps) * pl + (c % ps) : c; }
+
 // XCD-aware block order (MI355X: workgroups are dispatched round-robin over the 8
 // XCDs, each with its own L2): logical ids [k*nb/8, (k+1)*nb/8) all run on XCD k,
 // so consecutive logical blocks -- which the kernels make share input tiles --

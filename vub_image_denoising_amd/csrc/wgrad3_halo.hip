@@ -85,6 +85,13 @@ __global__ __launch_bounds__(NT, 2) void wgrad3_halo_kernel(rdn_wgrad_desc d, in
       sb[q] = 0.f;
     }
   }
+  // channel offsets of this thread's A and B units: the unit's channel group is the
+  // same in every iteration (NT is a multiple of both unit counts per pixel), so
+  // the channel-blocked decode (rdn_coff) runs once
+  const int a_cf = rdn_coff32(d.a_c0 + m0 + acg * VEC, (int)d.a_ps, (int)d.a_pl);
+  const int g_cf = GATE ? rdn_coff32(m0 + acg * VEC, (int)d.a_gate_ps, (int)d.a_gate_pl) : 0;
+  static_assert(NT % (CK / VEC) == 0, "fixed B channel group per thread");
+  const int b_cf = rdn_coff32(d.b_c0 + c0 + (tid % (CK / VEC)) * VEC, (int)d.b_ps, (int)d.b_pl);
   auto load_tile = [&](int t) {
     const int tx = t % tiles_x, r1 = t / tiles_x;
     const int ty = r1 % tiles_y, nimg = r1 / tiles_y;
@@ -99,8 +106,8 @@ __global__ __launch_bounds__(NT, 2) void wgrad3_halo_kernel(rdn_wgrad_desc d, in
         const int m = m0 + cu * VEC;
         if (yy < H && xx < W && m < d.mdim) {
           const int64_t pix = ((int64_t)nimg * H + yy) * W + xx;
-          v = *(const u32x4*)(A + pix * d.a_ps + d.a_c0 + m);
-          if constexpr (GATE) gv = *(const u32x4*)(G + pix * d.a_gate_ps + m);
+          v = *(const u32x4*)(A + pix * d.a_ps + a_cf);
+          if constexpr (GATE) gv = *(const u32x4*)(G + pix * d.a_gate_ps + g_cf);
         }
       }
       dreg[it] = v;
@@ -115,7 +122,7 @@ __global__ __launch_bounds__(NT, 2) void wgrad3_halo_kernel(rdn_wgrad_desc d, in
         const int hy = hp / (TW + 2), hx = hp - hy * (TW + 2);
         const int yy = y0 + hy - 1, xx = x0 + hx - 1;
         if (yy >= 0 && yy < H && xx >= 0 && xx < W)
-          v = *(const u32x4*)(Bx + (((int64_t)nimg * H + yy) * W + xx) * d.b_ps + d.b_c0 + c0 + cu * VEC);
+          v = *(const u32x4*)(Bx + (((int64_t)nimg * H + yy) * W + xx) * d.b_ps + b_cf);
       }
       hreg[it] = v;
     }
@@ -328,16 +335,18 @@ __global__ __launch_bounds__(NT, (BM * CK > 2560 ? 1 : 2)) void wgrad3_rows_kern
   // ---- per-thread unit geometry (tile-invariant)
   const int acg = tid % DU;                     // this thread's dY channel group
   const bool m_ok = m0 + acg * VEC < d.mdim;
-  int drel[D_IT], grel[GATE ? D_IT : 1], dlds[D_IT], dpix[D_IT];
+  const int a_cf = rdn_coff32(d.a_c0 + m0 + acg * VEC, (int)d.a_ps, (int)d.a_pl);   // channel-blocked decode, once
+  const int g_cf = GATE ? rdn_coff32(m0 + acg * VEC, (int)d.a_gate_ps, (int)d.a_gate_pl) : 0;
+  int drel[D_IT], grel[GATE ? D_IT : 1];
 #pragma unroll
   for (int it = 0; it < D_IT; ++it) {
-    const int u = tid + it * NT;
-    const int p = u / DU;
-    dpix[it] = p;
-    drel[it] = ((p / TW) * W + p % TW) * (int)d.a_ps + d.a_c0 + m0 + acg * VEC;
-    if constexpr (GATE) grel[it] = ((p / TW) * W + p % TW) * (int)d.a_gate_ps + m0 + acg * VEC;
-    dlds[it] = p * DROW + acg * 16;
+    const int p = (tid + it * NT) / DU;
+    drel[it] = ((p / TW) * W + p % TW) * (int)d.a_ps + a_cf;
+    if constexpr (GATE) grel[it] = ((p / TW) * W + p % TW) * (int)d.a_gate_ps + g_cf;
   }
+  // pixel of dY unit `it` and its LDS offset (constant divisors: no tables)
+  auto dpix = [&](int it) { return (tid + it * NT) / DU; };
+  auto dlds = [&](int it) { return dpix(it) * DROW + acg * 16; };
   constexpr bool HLIN = HROW == HU * 16;        // unpadded halo rows: LDS offset = unit * 16
   int hrel[H_IT], hlds[HLIN ? 1 : H_IT];
 #pragma unroll
@@ -345,7 +354,7 @@ __global__ __launch_bounds__(NT, (BM * CK > 2560 ? 1 : 2)) void wgrad3_rows_kern
     const int u = tid + it * NT;
     const int hp = u / HU, cu = u - hp * HU;
     const int hy = hp / (TW + 2), hx = hp - hy * (TW + 2);
-    hrel[it] = (hy * W + hx) * (int)d.b_ps + d.b_c0 + c0 + cu * VEC;
+    hrel[it] = (hy * W + hx) * (int)d.b_ps + rdn_coff32(d.b_c0 + c0 + cu * VEC, (int)d.b_ps, (int)d.b_pl);
     if constexpr (!HLIN) hlds[it] = hp * HROW + cu * 16;
   }
 
@@ -372,7 +381,7 @@ __global__ __launch_bounds__(NT, (BM * CK > 2560 ? 1 : 2)) void wgrad3_rows_kern
     const bf16* const gb = GATE ? G + pix0 * d.a_gate_ps : nullptr;
 #pragma unroll
     for (int it = 0; it < D_IT; ++it) {
-      const int p = dpix[it];
+      const int p = dpix(it);
       bool ok = m_ok && ((it + 1 < D_IT) || tid + it * NT < D_UNITS);
       if (!full) ok = ok && y0 + p / TW < H && x0 + p % TW < W;
       u32x4 v = {0u, 0u, 0u, 0u}, gv = {0u, 0u, 0u, 0u};
@@ -420,7 +429,7 @@ __global__ __launch_bounds__(NT, (BM * CK > 2560 ? 1 : 2)) void wgrad3_rows_kern
           for (int q = 0; q < VEC; ++q) sb[q] += dy[q];
         }
       }
-      *(u32x4*)(dyl + dlds[it]) = v;
+      *(u32x4*)(dyl + dlds(it)) = v;
     }
 #pragma unroll
     for (int it = 0; it < H_IT; ++it) {

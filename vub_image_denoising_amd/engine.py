@@ -122,6 +122,12 @@ WGRAD_STREAM = os.environ.get("RDN_WGRAD_STREAM", "1") != "0"
 WGRAD_SLOTS = max(2, int(os.environ.get("RDN_WGRAD_SLOTS", "4")))
 # bench.py's per-kernel profiling pass serialises the backward (isolated kernel times)
 SERIAL_BWD = False
+# channel-blocked ("planar") activation buffers: a level-l buffer is [C/cb, P, cb] with
+# cb = F_l/2 (one plane per dense-block growth slice), so a conv reading or writing a
+# channel slice touches only its planes (include/rdunet_hip.h, *_pl fields)
+PLANAR = os.environ.get("RDN_PLANAR", "1") != "0"
+# extra elements between two planes (keeps plane starts off power-of-two strides)
+PLANE_PAD = int(os.environ.get("RDN_PLANE_PAD", "0"))
 
 
 def find_flat(params):
@@ -369,17 +375,31 @@ class UNetEngine:
         self.P = [B * (Hh >> l) * (Ww >> l) for l in range(4)]
         self.grid = [(B, Hh >> l, Ww >> l) for l in range(4)]
         self.bufs = {}
+        self.geo = {}   # buffer name -> (pixel stride ps, plane stride pl); pl = 0: plain NHWC
+        F = [F0 << l for l in range(4)]
+
+        def alloc(name, lvl, ch):
+            cb = F[lvl] // 2
+            if PLANAR and name not in ("IN", "dIN") and not name.startswith("PRE_") and ch % cb == 0 and ch > cb:
+                pl = self.P[lvl] * cb + PLANE_PAD
+                t = torch.zeros(ch // cb, pl, dtype=dtype, device=dev)
+                self.geo[name] = (cb, pl)
+            else:
+                t = torch.zeros(self.P[lvl], ch, dtype=dtype, device=dev)
+                self.geo[name] = (ch, 0)
+            self.bufs[name] = t
+
         for name, (lvl, ch) in bufspec.items():
             if not train and name.startswith("PRE_"):
                 continue
-            self.bufs[name] = torch.zeros(self.P[lvl], ch, dtype=dtype, device=dev)
+            alloc(name, lvl, ch)
         self.named = dict(module.named_parameters())
         self._build_fwd()
         if train:
             for name, (lvl, ch) in bufspec.items():
                 if name.startswith("PRE_"):
                     continue
-                self.bufs["d" + name] = torch.zeros(self.P[lvl], ch, dtype=dtype, device=dev)
+                alloc("d" + name, lvl, ch)
             # weight gradients (wgrad + reduce) run on a side stream, overlapped with
             # the dgrad chain; the per-layer dYpre / PReLU-partial buffers they read
             # form a ring of SLOTS so the dgrad chain can run SLOTS layers ahead
@@ -401,6 +421,11 @@ class UNetEngine:
     def _buf(self, name):
         return self.bufs[name]
 
+    def _slice(self, sl):
+        """(pointer, ps, c0, pl) of a channel slice of a buffer."""
+        ps, pl = self.geo[sl.buf]
+        return self.bufs[sl.buf].data_ptr(), ps, sl.c0, pl
+
     def _build_fwd(self):
         lib = H.lib()
         for L in self.layers:
@@ -408,8 +433,7 @@ class UNetEngine:
             d.dtype = self.code
             n, h, w = self.grid[L.level]
             d.n, d.h, d.w = n, h, w
-            src = self._buf(L.src.buf)
-            d.x, d.x_ps, d.x_c0 = src.data_ptr(), src.shape[1], L.src.c0
+            d.x, d.x_ps, d.x_c0, d.x_pl = self._slice(L.src)
             packed = L.pack_fwd[8]
             d.wp, d.kp = packed.data_ptr(), packed.shape[1]
             d.bias = self.named[L.name + ".bias"].data_ptr()
@@ -438,12 +462,11 @@ class UNetEngine:
             if L.dst is None:
                 flags |= H.EPI_OUT_NCHW | H.EPI_RESID  # + inputs (Unet_model.py:166)
             else:
-                dst = self._buf(L.dst.buf)
-                d.out, d.out_ps, d.out_c0 = dst.data_ptr(), dst.shape[1], L.dst.c0
+                d.out, d.out_ps, d.out_c0, d.out_pl = self._slice(L.dst)
                 if L.resid is not None:
-                    r = self._buf(L.resid.buf)
                     flags |= H.EPI_RESID
-                    d.res, d.res_ps, d.res_c0, d.res_climit = r.data_ptr(), r.shape[1], L.resid.c0, L.resid_c
+                    d.res, d.res_ps, d.res_c0, d.res_pl = self._slice(L.resid)
+                    d.res_climit = L.resid_c
             d.flags = flags
             L.fwd_desc = d
 
@@ -483,8 +506,7 @@ class UNetEngine:
                 d.x_ps, d.cin = L.cout_pad, L.cout_pad
                 d.ncols = d.cout = L.cin
                 if fused:
-                    dd = self._buf(L.ddst.buf)
-                    d.x, d.x_ps, d.x_c0 = dd.data_ptr(), dd.shape[1], L.ddst.c0
+                    d.x, d.x_ps, d.x_c0, d.x_pl = self._slice(L.ddst)
                     d.gate, d.gate_ps, d.gate_alpha = pre.data_ptr(), pre.shape[1], alpha.data_ptr()
             elif L.kind == "down":       # per-pixel GEMM on the low-res grid, scattered to 2x2
                 n, h, w = self.grid[L.level]
@@ -498,14 +520,13 @@ class UNetEngine:
                 d.x_ps, d.cin = L.cout, L.cout
                 d.ncols = d.cout = L.cin
             d.n, d.h, d.w = n, h, w
-            dsrc = self._buf(L.dsrc.buf)
-            d.out, d.out_ps, d.out_c0 = dsrc.data_ptr(), dsrc.shape[1], L.dsrc.c0
+            d.out, d.out_ps, d.out_c0, d.out_pl = self._slice(L.dsrc)
             if L.accum:
                 flags |= H.EPI_ACCUM
             if L.resid is not None:      # d(x) += dOut through "out_3 + x" (Unet_model.py:89)
-                dd = self._buf(L.ddst.buf)
                 flags |= H.EPI_RESID
-                d.res, d.res_ps, d.res_c0, d.res_climit = dd.data_ptr(), dd.shape[1], L.ddst.c0, L.resid_c
+                d.res, d.res_ps, d.res_c0, d.res_pl = self._slice(L.ddst)
+                d.res_climit = L.resid_c
             d.flags = flags
             L.dgrad_desc = d
             # --- weight gradient
@@ -514,26 +535,25 @@ class UNetEngine:
             if L.kind == "c3":
                 n, h, w = self.grid[L.level]
                 wg.gather, wg.n, wg.h, wg.w, wg.hin, wg.win = H.RDN_G_CONV3, n, h, w, h, w
-                src = self._buf(L.src.buf)
                 wg.a, wg.a_ps, wg.a_c0, wg.mdim = dyp, L.cout_pad, 0, L.cout
-                wg.b, wg.b_ps, wg.b_c0, wg.ndim = src.data_ptr(), src.shape[1], L.src.c0, L.cin_pad
+                wg.b, wg.b_ps, wg.b_c0, wg.b_pl = self._slice(L.src)
+                wg.ndim = L.cin_pad
                 taps, ndim_real = 9, L.cin
                 if fused:
-                    dd = self._buf(L.ddst.buf)
-                    wg.a, wg.a_ps, wg.a_c0 = dd.data_ptr(), dd.shape[1], L.ddst.c0
+                    wg.a, wg.a_ps, wg.a_c0, wg.a_pl = self._slice(L.ddst)
                     wg.a_gate, wg.a_gate_ps, wg.a_gate_alpha = pre.data_ptr(), pre.shape[1], alpha.data_ptr()
             elif L.kind == "down":
                 n, h, w = self.grid[L.level]
                 wg.gather, wg.n, wg.h, wg.w, wg.hin, wg.win = H.RDN_G_S2, n, h, w, 2 * h, 2 * w
-                src = self._buf(L.src.buf)
                 wg.a, wg.a_ps, wg.a_c0, wg.mdim = dyp, L.cout, 0, L.cout
-                wg.b, wg.b_ps, wg.b_c0, wg.ndim = src.data_ptr(), src.shape[1], L.src.c0, L.cin
+                wg.b, wg.b_ps, wg.b_c0, wg.b_pl = self._slice(L.src)
+                wg.ndim = L.cin
                 taps, ndim_real = 4, L.cin
             else:
                 n, h, w = self.grid[L.level]
                 wg.gather, wg.n, wg.h, wg.w, wg.hin, wg.win = H.RDN_G_S2, n, h, w, 2 * h, 2 * w
-                src = self._buf(L.src.buf)
-                wg.a, wg.a_ps, wg.a_c0, wg.mdim = src.data_ptr(), src.shape[1], L.src.c0, L.cin
+                wg.a, wg.a_ps, wg.a_c0, wg.a_pl = self._slice(L.src)
+                wg.mdim = L.cin
                 wg.b, wg.b_ps, wg.b_c0, wg.ndim = dyp, L.cout, 0, L.cout
                 taps, ndim_real = 4, L.cout
             wg.splits = 0
@@ -685,13 +705,13 @@ class UNetEngine:
                 if side is not None and b >= self.slots:
                     main.wait_event(rev[b - self.slots].extra["ev_done"])
                 if L.ddst is None:
-                    rc = lib.rdn_prelu_bwd(self.code, P, n, h, w, L.cout, L.cout_pad, None, 0, 0, dy.data_ptr(),
+                    rc = lib.rdn_prelu_bwd(self.code, P, n, h, w, L.cout, L.cout_pad, None, 0, 0, 0, dy.data_ptr(),
                                            pre.data_ptr(), pre.shape[1], self.named[L.act + ".weight"].data_ptr(),
                                            dyp, None, None, pws, st)
                 else:
-                    dd = self.bufs[L.ddst.buf]
-                    rc = lib.rdn_prelu_bwd(self.code, P, n, h, w, L.cout, L.cout_pad, dd.data_ptr(), dd.shape[1],
-                                           L.ddst.c0, None, pre.data_ptr(), pre.shape[1],
+                    dd_ptr, dd_ps, dd_c0, dd_pl = self._slice(L.ddst)
+                    rc = lib.rdn_prelu_bwd(self.code, P, n, h, w, L.cout, L.cout_pad, dd_ptr, dd_ps,
+                                           dd_c0, dd_pl, None, pre.data_ptr(), pre.shape[1],
                                            self.named[L.act + ".weight"].data_ptr(), dyp, None, None, pws, st)
             if rc:
                 H.check(rc, f"prelu_bwd[{L.name}]")
@@ -732,7 +752,7 @@ class UNetEngine:
             return None
         dx = dy.clone()  # global residual: output + inputs (Unet_model.py:166)
         dIN = self.bufs["dIN"]
-        H.check(lib.rdn_nhwc_to_nchw(self.code, dIN.data_ptr(), dIN.shape[1], 0, self.B, self.cin_img, self.H, self.W,
+        H.check(lib.rdn_nhwc_to_nchw(self.code, dIN.data_ptr(), dIN.shape[1], 0, 0, self.B, self.cin_img, self.H, self.W,
                                      dx.data_ptr(), 1, st), "nhwc_to_nchw")
         return dx
 
