@@ -41,6 +41,7 @@ import torch.distributed as dist  # noqa: E402
 PEAK_BF16_TFLOPS = 2500.0   # dense MFMA (MI355X_MICROARCH.md chip table)
 PEAK_F32_TFLOPS = 157.3
 PEAK_HBM_GBS = 8000.0
+MEASURED_HBM_GBS = 6290.0   # float4 copy on MI355X (MI355X_MICROARCH.md chip table)
 
 
 class EventTracer:
@@ -91,8 +92,31 @@ class EventTracer:
         return by
 
 
-def cpu_baseline(seconds=12.0, batch=2, size=256):
-    """The CPU oracle's train step (fp32, torch aten on the host cores)."""
+def extra_configs(dev, args):
+    """The same train step at north_star's batch 32 (bf16, with the residual-dense
+    conv path's HBM roofline from a serialised profiling pass) and at the
+    reference's own precision (fp32, batch 16).  Rank 0 of a 1-GPU run only."""
+    out = {}
+    for key, batch, dtype, warm, steps in (("b32", 32, "bf16", 3, args.steps), ("fp32", 16, "fp32", 2, 6)):
+        _log(f"extra config {key}: batch {batch} {dtype}")
+        tr = Trainer(dev, batch, args.size, args.base_filters, dtype)
+        for i in range(warm):
+            tr.step(i)
+        prof = tr.profile() if key == "b32" else None
+        el, loss = tr.timed(steps)
+        r = {"per_gpu_batch": batch, "dtype": dtype, "steps": steps, "ms_per_step": round(el * 1e3 / steps, 3),
+             "images_per_s": round(batch * steps / el, 2), "final_loss": round(loss.item(), 5)}
+        if prof is not None:
+            r["dense_conv_path"] = dense_conv_path(prof, batch)
+        out[key] = r
+        del tr, prof
+        torch.cuda.empty_cache()
+    return out
+
+
+def cpu_baseline(seconds=12.0, batch=16, size=256):
+    """The CPU oracle's train step (fp32, torch aten on the host cores), at the
+    headline's per-GPU batch: one warm-up step, then whole steps until `seconds`."""
     from oracle import rdunet_ref as R
     from oracle.weights import make_params
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
@@ -274,6 +298,99 @@ def metrics_bench(dev, n=64, size=256):
             "note": "per-block skimage on the host (reference) is not timed here"}
 
 
+class Trainer:
+    """One RDUNet_T train step (the timed unit) for a (per-GPU batch, dtype):
+    synthetic seeded data resident in HBM, FusedAdamW every step."""
+
+    def __init__(self, dev, batch, size, base_filters, dtype, rank=0, world=1):
+        import vub_image_denoising_amd as vm
+        from vub_image_denoising_amd.ddp import GradSync
+        from vub_image_denoising_amd.diffusion_RDUnet import DiffusionModel, train_step_device
+        from vub_image_denoising_amd.optim import FusedAdamW
+        self.batch = batch
+        torch.manual_seed(1234)
+        self.unet = vm.RDUNet_T(base_filters=base_filters).to(dev).set_compute_dtype(dtype)
+        self.model = DiffusionModel(self.unet, timesteps=20)
+        # synthetic data resident in HBM: one batch per sigma, rank-specific seed
+        gen = torch.Generator(device=dev).manual_seed(1234 + 7919 * rank)
+        self.batches = []
+        for sigma in (15.0, 25.0, 50.0):
+            clean = torch.rand(batch, 3, size, size, generator=gen, device=dev) * 2 - 1
+            noisy = clean + (sigma / 255.0 * 2.0) * torch.randn(batch, 3, size, size, generator=gen, device=dev)
+            self.batches.append((noisy, clean))
+        torch.manual_seed(99 + rank)  # t draws (torch.randint on the device)
+        self._train_step = train_step_device
+        self.opt = None
+        self.step(0)  # builds the flat parameter buffer and the engine
+        self.opt = FusedAdamW(self.model.parameters(), lr=1e-4, weight_decay=1e-4)
+        if world > 1:
+            self.unet._rdn_flat.grad_sync = GradSync(self.unet._rdn_flat, bucket_mb=25.0)
+
+    def step(self, i):
+        noisy, clean = self.batches[i % 3]
+        opt = self.opt if self.opt is not None else self
+        loss = self._train_step(self.model, clean, noisy, opt, "uniform", 1.0)
+        if self.opt is not None:
+            self.opt.step()
+        return loss
+
+    def zero_grad(self, set_to_none=True):   # stands in for the optimizer on the first step
+        for p in self.model.parameters():
+            p.grad = None
+
+    def profile(self):
+        """One step with every conv launch timed alone (backward serialised)."""
+        from vub_image_denoising_amd import engine as E
+        prof = EventTracer()
+        E.TRACER, E.SERIAL_BWD = prof, True
+        try:
+            self.step(0)
+        finally:
+            E.TRACER, E.SERIAL_BWD = None, False
+        return prof
+
+    def timed(self, steps, world=1, tracer=None):
+        from vub_image_denoising_amd import engine as E
+        E.TRACER = tracer
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            loss = self.step(i)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        E.TRACER = None
+        return el, loss
+
+
+DENSE_LEVELS = (0, 1)
+
+
+def dense_conv_path(prof, batch):
+    """HBM roofline of north_star's "residual-dense conv path": the 3x3 convs of the
+    level-0/1 DenoisingBlocks (Unet_model.py:72-89; block_0_* / block_1_* conv_0..3)
+    in forward, input gradient and weight gradient.  achieved = their algorithmic
+    bytes (each operand read once, each output written once, engine._build_info) /
+    their summed isolated kernel time of one step."""
+    import re
+    byts, ms, n = 0.0, 0.0, 0
+    for info, s, e in prof.records:
+        m = re.match(r"block_(\d)_\d\.conv_\d$", info[1])
+        if m and int(m.group(1)) in DENSE_LEVELS:
+            byts += info[4]
+            ms += s.elapsed_time(e)
+            n += 1
+    gbs = byts / (ms * 1e-3) / 1e9
+    return {"batch": batch, "levels": list(DENSE_LEVELS), "launches": n, "bytes_per_step_gb": round(byts / 1e9, 3),
+            "kernel_ms_per_step": round(ms, 3), "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": round(gbs / PEAK_HBM_GBS, 4),
+            "frac_of_measured_copy_bw": round(gbs / MEASURED_HBM_GBS, 4),
+            "note": "isolated (serialised-backward) launch times; bytes incl. the fused PReLU-backward gate reads"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -288,6 +405,7 @@ def main():
     ap.add_argument("--layer-report", default="", help="write a per-kernel time table (json) here")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes (roofline.traffic)")
     ap.add_argument("--no-inference", action="store_true", help="skip the sampler measurements")
+    ap.add_argument("--no-extra", action="store_true", help="skip the batch-32 and fp32 train-step lines")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
@@ -299,59 +417,14 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    import vub_image_denoising_amd as vm
-    from vub_image_denoising_amd import engine as E
-    from vub_image_denoising_amd.ddp import GradSync
-    from vub_image_denoising_amd.diffusion_RDUnet import DiffusionModel, train_step_device
-    from vub_image_denoising_amd.optim import FusedAdamW
-
-    torch.manual_seed(1234)
-    unet = vm.RDUNet_T(base_filters=args.base_filters).to(dev).set_compute_dtype(args.dtype)
-    model = DiffusionModel(unet, timesteps=20)
-    # synthetic data resident in HBM: one batch per sigma, rank-specific seed
-    gen = torch.Generator(device=dev).manual_seed(1234 + 7919 * rank)
-    batches = []
-    for sigma in (15.0, 25.0, 50.0):
-        clean = torch.rand(args.batch, 3, args.size, args.size, generator=gen, device=dev) * 2 - 1
-        noisy = clean + (sigma / 255.0 * 2.0) * torch.randn(args.batch, 3, args.size, args.size, generator=gen,
-                                                            device=dev)
-        batches.append((noisy, clean))
-    torch.manual_seed(99 + rank)  # t draws (torch.randint on the device)
-
-    opt = None
-
-    def step(i):
-        nonlocal opt
-        noisy, clean = batches[i % 3]
-        loss = train_step_device(model, clean, noisy, opt if opt is not None else _NoOpt(), "uniform", 1.0)
-        if opt is None:
-            return loss
-        opt.step()
-        return loss
-
-    class _NoOpt:
-        def zero_grad(self, set_to_none=True):
-            for p in model.parameters():
-                p.grad = None
-
-    step(0)  # builds the flat parameter buffer and the engine
-    fp = unet._rdn_flat
-    opt = FusedAdamW(model.parameters(), lr=1e-4, weight_decay=1e-4)
-    if world > 1:
-        fp.grad_sync = GradSync(fp, bucket_mb=25.0)
-
+    tr = Trainer(dev, args.batch, args.size, args.base_filters, args.dtype, rank, world)
     for i in range(args.warmup):
-        step(i)
+        tr.step(i)
     torch.cuda.synchronize()
 
     # per-kernel profile pass (not timed): find the dominant kernel instantiation
     # (backward serialised: every launch timed alone, not beside the other stream)
-    prof = EventTracer()
-    E.TRACER = prof
-    E.SERIAL_BWD = True
-    step(0)
-    E.SERIAL_BWD = False
-    E.TRACER = None
+    prof = tr.profile()
     table = prof.summary()
     dom = max(table, key=lambda k: table[k]["ms"])
     if rank == 0 and args.layer_report:
@@ -363,18 +436,7 @@ def main():
 
     # timed region: events only around the dominant kernel's launches
     live = EventTracer(keys={dom})
-    E.TRACER = live
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        loss = step(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    E.TRACER = None
+    el, loss = tr.timed(args.steps, world, live)
     if world > 1:
         tt = torch.tensor([el], device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -418,9 +480,17 @@ def main():
                                       else (bytes_per / (iso_ms * 1e-3) / 1e9 / PEAK_HBM_GBS), 4)
         roof["launches_per_step"] = d["n"] // args.steps
         roof["share_of_step"] = round(d["ms"] / (el * 1e3), 4)
+        roof[f"dense_conv_path_b{args.batch}"] = dense_conv_path(prof, args.batch)
+        extra = None
+        if world == 1 and not (args.no_extra or args.pmc_child):
+            del tr
+            torch.cuda.empty_cache()
+            extra = extra_configs(dev, args)
+            roof["dense_conv_path"] = extra["b32"].pop("dense_conv_path")
         if not (args.no_cpu_baseline or args.pmc_child):
             _log("CPU baseline")
-        cpu = None if (args.no_cpu_baseline or args.pmc_child) else cpu_baseline(args.cpu_seconds)
+        cpu = None if (args.no_cpu_baseline or args.pmc_child) else cpu_baseline(args.cpu_seconds, args.batch,
+                                                                                 args.size)
         infer = None
         if not (args.no_inference or args.pmc_child) and world == 1:
             _log("sampler measurements")
@@ -444,6 +514,9 @@ def main():
                        "image": [3, args.size, args.size], "timesteps": 20,
                        "parallelism": f"dp{world}", "optimizer_step": "every step",
                        "final_loss": round(loss_v, 5)},
+            "b32_images_per_s": extra["b32"]["images_per_s"] if extra else None,
+            "fp32_images_per_s": extra["fp32"]["images_per_s"] if extra else None,
+            "extra_configs": extra,
             "roofline": roof,
             "cpu_baseline": cpu,
             "inference": infer,

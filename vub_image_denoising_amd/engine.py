@@ -625,11 +625,14 @@ class UNetEngine:
                               (Pout * L.cout if L.resid is not None else 0))
             info = {"fwd": ("fwd", L.name, self._kernel_key(L.fwd_desc), 2 * macs, fwd_bytes)}
             if self.train:
-                dg_bytes = es * (Pout * L.cout + Pin * L.cin * (2 if L.accum else 1) +
+                # a fused PReLU backward (gate in the loader) also reads the saved
+                # PReLU input of the output slice
+                gate = Pout * L.cout if L.extra.get("fused") else 0
+                dg_bytes = es * (Pout * L.cout + gate + Pin * L.cin * (2 if L.accum else 1) +
                                  (Pin * L.resid_c if L.resid is not None else 0))
                 info["dgrad"] = ("dgrad", L.name, self._kernel_key(L.dgrad_desc), 2 * macs, dg_bytes)
                 info["wgrad"] = ("wgrad", L.name, self._wgrad_key(L.wgrad_desc), 2 * macs,
-                                 es * (Pout * L.cout + Pin * L.cin))
+                                 es * (Pout * L.cout + gate + Pin * L.cin))
             L.extra["info"] = info
 
     # ------------------------------------------------------------------
