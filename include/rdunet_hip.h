@@ -210,11 +210,17 @@ int rdn_sqnorm(const float* g, int64_t count, float max_norm, float* ws, float* 
 int rdn_clip_scale(float* g, int64_t count, const float* coef, void* stream);
 
 /* torch.optim.Adam(W) step over flat fp32 buffers.  decoupled = 1 -> AdamW
-   (p *= 1 - lr*wd), 0 -> Adam L2 (g += wd*p).  bc1 = 1-beta1^t, bc2 = 1-beta2^t.
-   grad_scale multiplies g first (e.g. 1/world_size). */
+   (p *= 1 - lr*wd), 0 -> Adam L2 (g += wd*p).  Hyperparameters come in double and
+   every derived scalar (1-beta, lr/(1-beta1^t), sqrt(1-beta2^t), 1-lr*wd) is rounded
+   to fp32 from double, as torch's single-tensor Adam does.  `step` (>= 1) is the
+   step number t; when step_dev != NULL it is read from device memory instead (a
+   graph-replayable optimizer step; advance it with rdn_counter_inc).  grad_scale
+   multiplies g first (e.g. 1/world_size). */
 int rdn_adam_step(float* p, const float* g, float* m, float* v, int64_t count,
-                  float lr, float beta1, float beta2, float eps, float wd, int32_t decoupled,
-                  float bc1, float bc2, float grad_scale, void* stream);
+                  double lr, double beta1, double beta2, double eps, double wd, int32_t decoupled,
+                  int64_t step, const int64_t* step_dev, float grad_scale, void* stream);
+/* *counter += 1 on the device (one thread; stream-ordered) */
+int rdn_counter_inc(int64_t* counter, void* stream);
 
 /* improved_sampling update: x = x - (c1*f1 + a*y) + (c2*f2 + ap*y), with c1 = 1-a and
    c2 = 1-ap rounded on the host exactly as the reference's Python scalars are */

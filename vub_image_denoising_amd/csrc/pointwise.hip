@@ -373,26 +373,56 @@ __global__ void scale_kernel(float* __restrict__ g, int64_t n, const float* __re
     g[i] *= c;
 }
 
-// torch.optim.Adam/AdamW single-tensor math (torch/optim/adam.py, _single_tensor_adam):
-//   AdamW: p *= 1 - lr*wd ; Adam: g += wd*p
-//   m = b1*m + (1-b1)*g ; v = b2*v + (1-b2)*g*g
-//   p -= (lr/bc1) * m / (sqrt(v)/sqrt(bc2) + eps)
+// torch.optim.Adam/AdamW single-tensor math (torch/optim/adam.py, _single_tensor_adam),
+// with every scalar rounded to fp32 from the same double torch computes it in:
+//   AdamW: p *= (1 - lr*wd) ; Adam: g += wd*p
+//   m = lerp(m, g, 1-b1) ; v = v*b2 + (1-b2)*g*g
+//   p += -(lr/bc1) * m / (sqrt(v)/sqrt(bc2) + eps),  bc_i = 1 - b_i^step
+struct AdamScalars {
+  float decay, wd, omb1, b2, omb2, step_size, bc2s, eps;
+};
+__host__ __device__ inline AdamScalars adam_scalars(double lr, double b1, double b2, double eps, double wd,
+                                                    int decoupled, double step) {
+  AdamScalars a;
+  const double bc1 = 1.0 - pow(b1, step), bc2 = 1.0 - pow(b2, step);
+  a.decay = decoupled ? (float)(1.0 - lr * wd) : 1.f;
+  a.wd = decoupled ? 0.f : (float)wd;
+  a.omb1 = (float)(1.0 - b1);
+  a.b2 = (float)b2;
+  a.omb2 = (float)(1.0 - b2);
+  a.step_size = (float)(lr / bc1);
+  a.bc2s = (float)sqrt(bc2);
+  a.eps = (float)eps;
+  return a;
+}
+
+// host_sc: the scalars of a host-known step; with step_dev != nullptr the step count
+// is read from device memory (graph-replayable optimizer step) and the scalars are
+// derived on the device in double, exactly as on the host
 __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
-                            float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps, float wd,
-                            int decoupled, float bc1, float bc2s, float gs) {
-  const float step = lr / bc1;
+                            float* __restrict__ v, int64_t n, AdamScalars host_sc, const int64_t* __restrict__ step_dev,
+                            double lr, double b1, double b2, double eps, double wd, int decoupled, float gs) {
+  __shared__ AdamScalars sc_s;
+  AdamScalars sc = host_sc;
+  if (step_dev) {
+    if (threadIdx.x == 0) sc_s = adam_scalars(lr, b1, b2, eps, wd, decoupled, (double)*step_dev);
+    __syncthreads();
+    sc = sc_s;
+  }
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     float pi = p[i], gi = g[i] * gs;
-    if (decoupled) pi *= 1.f - lr * wd;
-    else gi += wd * pi;
-    const float mi = m[i] + (gi - m[i]) * (1.f - b1);   // lerp form used by torch
-    const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+    pi *= sc.decay;
+    gi += sc.wd * pi;
+    const float mi = m[i] + (gi - m[i]) * sc.omb1;   // lerp form used by torch
+    const float vi = v[i] * sc.b2 + sc.omb2 * gi * gi;
     m[i] = mi;
     v[i] = vi;
-    pi -= step * (mi / (sqrtf(vi) / bc2s + eps));
+    pi += -sc.step_size * (mi / (sqrtf(vi) / sc.bc2s + sc.eps));
     p[i] = pi;
   }
 }
+
+__global__ void counter_inc_kernel(int64_t* c) { *c += 1; }
 
 // x_tilde = (1-a)*f1 + a*y; x_tilde_prev = (1-ap)*f2 + ap*y; x = x - x_tilde + x_tilde_prev
 // (diffusion_RDUnet.py:45-49), each product rounded separately as torch does.
@@ -572,13 +602,24 @@ extern "C" int rdn_clip_scale(float* g, int64_t count, const float* coef, void* 
   return rdn_check_launch("rdn_clip_scale");
 }
 
-extern "C" int rdn_adam_step(float* p, const float* g, float* m, float* v, int64_t count, float lr, float beta1,
-                             float beta2, float eps, float wd, int32_t decoupled, float bc1, float bc2, float grad_scale,
-                             void* stream) {
-  if (!p || !g || !m || !v || count <= 0 || bc1 <= 0.f || bc2 <= 0.f) { rdn_set_error("rdn_adam_step: bad arguments"); return RDN_E_ARG; }
-  adam_kernel<<<grid_for(count, 256 * 4), 256, 0, RDN_STREAM>>>(p, g, m, v, count, lr, beta1, beta2, eps, wd, decoupled, bc1,
-                                                               sqrtf(bc2), grad_scale);
+extern "C" int rdn_adam_step(float* p, const float* g, float* m, float* v, int64_t count, double lr, double beta1,
+                             double beta2, double eps, double wd, int32_t decoupled, int64_t step,
+                             const int64_t* step_dev, float grad_scale, void* stream) {
+  if (!p || !g || !m || !v || count <= 0 || (!step_dev && step < 1) || beta1 < 0 || beta1 >= 1 || beta2 < 0 ||
+      beta2 >= 1) {
+    rdn_set_error("rdn_adam_step: bad arguments");
+    return RDN_E_ARG;
+  }
+  const AdamScalars sc = adam_scalars(lr, beta1, beta2, eps, wd, decoupled, (double)(step < 1 ? 1 : step));
+  adam_kernel<<<grid_for(count, 256 * 4), 256, 0, RDN_STREAM>>>(p, g, m, v, count, sc, step_dev, lr, beta1, beta2, eps,
+                                                               wd, decoupled, grad_scale);
   return rdn_check_launch("rdn_adam_step");
+}
+
+extern "C" int rdn_counter_inc(int64_t* counter, void* stream) {
+  if (!counter) { rdn_set_error("rdn_counter_inc: null"); return RDN_E_ARG; }
+  counter_inc_kernel<<<1, 1, 0, RDN_STREAM>>>(counter);
+  return rdn_check_launch("rdn_counter_inc");
 }
 
 extern "C" int rdn_sampling_combine(float* x, const float* f1, const float* f2, const float* y, int64_t count, float c1,

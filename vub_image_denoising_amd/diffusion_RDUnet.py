@@ -81,13 +81,7 @@ def _draw_t(batch_size, timesteps, distribution_choice, dev):
     return torch.randint(0, timesteps + 1, (batch_size,), device=dev).float()
 
 
-def train_step_device(model, clean_images, noisy_images, optimizer, distribution_choice='uniform',
-                      clip_value=0.1, t=None, zero_grad=True):
-    """The body of train_step_checkpointed without the host sync: returns the
-    loss as a device tensor.  ``t`` (integer steps, [B]) overrides the draw."""
-    model.train()
-    if zero_grad:
-        optimizer.zero_grad()
+def _forward_loss(model, clean_images, noisy_images, distribution_choice, t):
     B = clean_images.size(0)
     T = model.timesteps
     if t is None:
@@ -96,10 +90,37 @@ def train_step_device(model, clean_images, noisy_images, optimizer, distribution
     interpolated = Fn.interpolate(clean_images, noisy_images, t_normalized)            # :99-100
     t_tensor = t_normalized.view(B, 1, 1, 1).expand(-1, 1, clean_images.size(2), clean_images.size(3))  # :93
     denoised = model.unet(interpolated, t_tensor)                                      # :106
-    loss = combined_loss(denoised, clean_images)                                       # :109
+    return combined_loss(denoised, clean_images)                                       # :109
+
+
+def train_step_device(model, clean_images, noisy_images, optimizer, distribution_choice='uniform',
+                      clip_value=0.1, t=None, zero_grad=True, clip=True):
+    """The body of train_step_checkpointed without the host sync: returns the
+    loss as a device tensor.  ``t`` (integer steps, [B]) overrides the draw.
+    ``zero_grad=False, clip=False`` accumulates into the existing gradients
+    (the fixed accumulation mode of run_epochs)."""
+    model.train()
+    if zero_grad:
+        optimizer.zero_grad()
+    loss = _forward_loss(model, clean_images, noisy_images, distribution_choice, t)
     loss.backward()                                                                    # :110
-    Fn.clip_grad_norm_(model.parameters(), clip_value)                                 # :113
+    if clip:
+        Fn.clip_grad_norm_(model.parameters(), clip_value)                             # :113
     return loss
+
+
+def forward_step_device(model, clean_images, noisy_images, distribution_choice='uniform', t=None, need_loss=True):
+    """A train step whose gradient the reference throws away (diffusion_RDUnet.py:78:
+    the next step's zero_grad): the same timestep draw (so the RNG streams stay the
+    reference's) and, when the loss is logged, the same forward + loss without
+    saved activations; no backward, no clip, no gradient all-reduce."""
+    if not need_loss:
+        if t is None:
+            _draw_t(clean_images.size(0), model.timesteps, distribution_choice, clean_images.device)
+        return None
+    model.train()
+    with torch.no_grad():
+        return _forward_loss(model, clean_images, noisy_images, distribution_choice, t)
 
 
 def train_step_checkpointed(model, clean_images, noisy_images, optimizer, accumulation_steps,
@@ -116,21 +137,40 @@ def train_step_checkpointed(model, clean_images, noisy_images, optimizer, accumu
 
 def train_model_checkpointed(model, train_loader, val_loader, optimizer, scheduler, writer, output_dir,
                              distribution_choice='uniform', num_epochs=10, start_epoch=0, accumulation_steps=4,
-                             clip_value=1.0, log_every=1):
+                             clip_value=1.0, log_every=1, accumulation='reference'):
     """diffusion_RDUnet.py:117-178: epochs of train steps with the reference's
     every-``accumulation_steps`` optimizer step, one-batch improved_sampling
     validation, scheduler step and a checkpoint dict per epoch.  ``log_every``
-    > 1 rate-limits the per-batch ``loss.item()`` host sync."""
+    > 1 rate-limits the per-batch ``loss.item()`` host sync; ``accumulation``
+    selects the reference's update rule or the fixed one (see run_epochs)."""
     run_epochs(model, train_loader, val_loader, optimizer, scheduler, writer, output_dir, distribution_choice,
                num_epochs, start_epoch, accumulation_steps, clip_value, log_every,
-               sample=lambda m, x: m.improved_sampling(x))
+               sample=lambda m, x: m.improved_sampling(x), accumulation=accumulation)
+
+
+ACCUMULATION_MODES = ("reference", "fixed")
 
 
 def run_epochs(model, train_loader, val_loader, optimizer, scheduler, writer, output_dir, distribution_choice,
-               num_epochs, start_epoch, accumulation_steps, clip_value, log_every, sample):
+               num_epochs, start_epoch, accumulation_steps, clip_value, log_every, sample, accumulation='reference',
+               skip_discarded=True):
     """The epoch loop shared by the three reference trainers (diffusion_RDUnet.py:117-178,
     main_diffusion_RDUnet.py:275-336, diffusion_RDUnet_direct.py:266-327); they
-    differ only in the validation sampler and the checkpoint directory."""
+    differ only in the validation sampler and the checkpoint directory.
+
+    accumulation='reference' keeps the reference's update rule:
+    train_step_checkpointed zeroes the gradients at its top (:78), so only the
+    clipped gradient of every ``accumulation_steps``-th batch reaches
+    ``optimizer.step()`` (:126-128).  The other batches' backward, clip and (DDP)
+    all-reduce are skipped -- their gradient is discarded by the reference -- while
+    their timestep draw and, when logged, their forward loss still run, so the
+    parameters are the reference's bit for bit at a third of those batches' cost.
+    accumulation='fixed' accumulates the gradients of ``accumulation_steps``
+    batches and clips + steps once (the rule of UNet/RDUNet_model.py:201-215).
+    ``skip_discarded=False`` runs the discarded backward passes anyway (the
+    reference's literal work; tests compare the two bit for bit)."""
+    if accumulation not in ACCUMULATION_MODES:
+        raise ValueError(f"accumulation must be one of {ACCUMULATION_MODES}, got {accumulation!r}")
     dev = next(model.parameters()).device
     for epoch in range(start_epoch, num_epochs):
         model.train()
@@ -138,11 +178,23 @@ def run_epochs(model, train_loader, val_loader, optimizer, scheduler, writer, ou
         n_batches = len(train_loader) if hasattr(train_loader, "__len__") else 0
         for batch_idx, (noisy_images, clean_images) in enumerate(train_loader):
             noisy_images, clean_images = noisy_images.to(dev), clean_images.to(dev)
-            loss_t = train_step_device(model, clean_images, noisy_images, optimizer, distribution_choice, clip_value)
-            if (batch_idx + 1) % accumulation_steps == 0:
+            step_now = (batch_idx + 1) % accumulation_steps == 0
+            log_now = batch_idx % log_every == 0
+            if accumulation == 'fixed':
+                loss_t = train_step_device(model, clean_images, noisy_images, optimizer, distribution_choice,
+                                           clip_value, zero_grad=False, clip=False)
+                if step_now:
+                    Fn.clip_grad_norm_(model.parameters(), clip_value)
+            elif step_now or not skip_discarded:
+                loss_t = train_step_device(model, clean_images, noisy_images, optimizer, distribution_choice,
+                                           clip_value)
+            else:
+                loss_t = forward_step_device(model, clean_images, noisy_images, distribution_choice,
+                                             need_loss=log_now)
+            if step_now:
                 optimizer.step()
                 optimizer.zero_grad()
-            if batch_idx % log_every == 0:
+            if log_now:
                 loss = loss_t.item()
                 print(f"Epoch [{epoch + 1}/{num_epochs}], Batch [{batch_idx + 1}/{n_batches}], Loss: {loss:.4f}")
                 if writer is not None:
@@ -232,7 +284,8 @@ def train(args, train_loader=None, val_loader=None):
     optimizer, scheduler = make_optimizer(args, model.parameters())
     start_epoch = load_checkpoint(model, optimizer, scheduler, args.checkpoint_path)
     train_model_checkpointed(model, train_loader, val_loader, optimizer, scheduler, writer, args.output_dir,
-                             args.distribution_choice, num_epochs=args.num_epochs, start_epoch=start_epoch)
+                             args.distribution_choice, num_epochs=args.num_epochs, start_epoch=start_epoch,
+                             accumulation=getattr(args, "accumulation", "reference"))
     final_model_path = os.path.join(args.output_dir, "diffusion_RDUNet_model_checkpointed_final.pth")
     torch.save(model.state_dict(), final_model_path)
     print(f"Final model saved at {final_model_path}")
@@ -260,6 +313,9 @@ def build_parser():
     parser.add_argument('--weight_decay', type=float, default=1e-4)
     parser.add_argument('--distribution_choice', type=str, default='uniform', choices=['uniform', 'biased'])
     parser.add_argument('--dtype', type=str, default='fp32', choices=['fp32', 'bf16'])
+    parser.add_argument('--accumulation', type=str, default='reference', choices=list(ACCUMULATION_MODES),
+                        help="reference: only every 4th batch's gradient is applied (the reference's rule, "
+                             "without the discarded backward passes); fixed: accumulate 4 batches")
     return parser
 
 

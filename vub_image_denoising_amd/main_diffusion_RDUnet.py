@@ -52,10 +52,10 @@ def _sample(model, x):
 
 
 def train_model_checkpointed(model, train_loader, val_loader, optimizer, scheduler, writer, num_epochs=10,
-                             start_epoch=0, accumulation_steps=4, clip_value=1.0):
+                             start_epoch=0, accumulation_steps=4, clip_value=1.0, *, accumulation='reference'):
     """main_diffusion_RDUnet.py:275-336."""
     run_epochs(model, train_loader, val_loader, optimizer, scheduler, writer, CHECKPOINT_DIR, 'uniform', num_epochs,
-               start_epoch, accumulation_steps, clip_value, 1, sample=_sample)
+               start_epoch, accumulation_steps, clip_value, 1, sample=_sample, accumulation=accumulation)
 
 
 def load_checkpoint(model, optimizer, scheduler, checkpoint_path):

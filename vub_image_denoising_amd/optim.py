@@ -5,7 +5,9 @@ Same update as ``torch.optim.Adam`` / ``AdamW`` (the optimizers of
 diffusion_RDUnet.py:264-268 and main_diffusion_RDUnet.py:230), same
 ``param_groups`` (so LR schedulers work) and a ``state_dict`` in torch's
 per-parameter format (``step``, ``exp_avg``, ``exp_avg_sq``), whose moment
-tensors are views of the flat moment buffers.
+tensors are views of the flat moment buffers.  ``load_state_dict`` restores the
+moments and the step count into those buffers, so a resumed run continues
+bit-identically (diffusion_RDUnet.py:180-193 resume path).
 """
 from __future__ import annotations
 
@@ -34,16 +36,40 @@ class FusedAdam(torch.optim.Optimizer):
             raise RuntimeError("FusedAdam needs the parameters of one GPU RDUNet (run a forward/backward first); "
                                "use torch.optim.Adam(W) otherwise")
         if self._fp is not fp:
+            # moments already in self.state (a load_state_dict before the first step,
+            # or a previous flat buffer) are carried over into the new flat buffers
+            old = {p: self.state[p] for p in fp.params if p in self.state}
             self._fp = fp
             self._m = torch.zeros_like(fp.flat)
             self._v = torch.zeros_like(fp.flat)
-            self._step = 0
             self._steps = torch.zeros((), dtype=torch.float32)
+            steps = set()
             for p, off in zip(fp.params, fp.offsets):
                 n = p.numel()
-                self.state[p] = {"step": self._steps, "exp_avg": self._m[off:off + n].view_as(p),
-                                 "exp_avg_sq": self._v[off:off + n].view_as(p)}
+                st = old.get(p)
+                if st and "exp_avg" in st:
+                    self._m[off:off + n].copy_(st["exp_avg"].reshape(-1))
+                    self._v[off:off + n].copy_(st["exp_avg_sq"].reshape(-1))
+                    steps.add(int(float(st["step"])))
+            if len(steps) > 1:
+                raise RuntimeError(f"FusedAdam: parameters were saved at different step counts {sorted(steps)}")
+            self._step = steps.pop() if steps else 0
+            self._steps.fill_(self._step)
+            self._views()
         return fp
+
+    def _views(self):
+        fp = self._fp
+        for p, off in zip(fp.params, fp.offsets):
+            n = p.numel()
+            self.state[p] = {"step": self._steps, "exp_avg": self._m[off:off + n].view_as(p),
+                             "exp_avg_sq": self._v[off:off + n].view_as(p)}
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        if self._fp is not None:          # already bound: rebind, copying the loaded state in
+            self._fp = None
+            self._bind()
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -55,9 +81,8 @@ class FusedAdam(torch.optim.Optimizer):
         b1, b2 = g["betas"]
         H.check(H.lib().rdn_adam_step(fp.flat.data_ptr(), fp.gflat.data_ptr(), self._m.data_ptr(), self._v.data_ptr(),
                                       fp.numel, float(g["lr"]), float(b1), float(b2), float(g["eps"]),
-                                      float(g["weight_decay"]), 1 if self.decoupled else 0,
-                                      1.0 - b1 ** self._step, 1.0 - b2 ** self._step, float(self.grad_scale),
-                                      H.stream_ptr()), "adam_step")
+                                      float(g["weight_decay"]), 1 if self.decoupled else 0, self._step, None,
+                                      float(self.grad_scale), H.stream_ptr()), "adam_step")
         fp.generation += 1  # weights changed behind torch's version counters: repack
         return loss
 
