@@ -262,7 +262,7 @@ def inference_bench(dev, base_filters=32):
     x64 = torch.rand(64, 3, 512, 512, device=dev) * 2 - 1
     g = SamplerGraph(dm, tuple(x64.shape), direct=True)
     t = timed(lambda: g(x64), 3)
-    eng = dm.unet._rdn_engines[(64, 512, 512, torch.bfloat16, False)]
+    eng = dm.unet._rdn_engines[(64, 512, 512, torch.bfloat16, False)][0]
     flops = sum(L.extra["info"]["fwd"][3] for L in eng.layers)
     res["direct_sampling_512_b64_bf16"] = {"ms_per_call": round(1e3 * t, 2), "images_per_s": round(64 / t, 1),
                                            "tflops": round(flops / t / 1e12, 1)}

@@ -21,6 +21,16 @@ PSNR is computed per image with the ``hyperparams_search.py:11-28`` convention
 (denormalise to [0, 1], 20*log10(1/RMSE), mean over images).  Target:
 |PSNR_gpu - PSNR_cpu| <= 0.05 dB.
 
+Paired design (``--seeds N``): every seed is one pair (same init, data, t draws
+for both legs); the statistic is the per-seed difference d_i = PSNR_gpu,i -
+PSNR_cpu,i, reported with its mean, standard deviation and a two-sided 95 %
+Student-t confidence interval.  Training is chaotic (rounding differences of a
+few ulps grow over the steps: the oracle against itself from 1e-6-perturbed
+weights differs by up to 0.2 dB per seed), so the interval, not one seed, is the
+evidence; it is narrower than +-0.05 dB at N ~ 12.  Each seed also checks the
+inference path alone: the GPU-trained weights denoise the held-out set on the
+GPU and in the oracle, d_inf = PSNR difference at identical weights.
+
   python scripts/psnr_parity.py [--steps 150] [--bf16] [--out profiles/x.json]
 """
 from __future__ import annotations
@@ -126,7 +136,23 @@ def run_gpu(args, params, data, dtype):
                          for i in range(0, ev_noisy.size(0), args.eval_batch)])
     losses = [float(v) for v in torch.stack(losses).cpu()]
     return {"psnr": psnr_per_image(den, ev_clean), "loss_first": losses[0], "loss_last": losses[-1],
-            "train_s": round(t_train, 2), "losses": losses}
+            "train_s": round(t_train, 2), "losses": losses,
+            "_state": {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}}
+
+
+def oracle_eval_psnr(args, state_dict, data):
+    """The oracle's improved_sampling + PSNR with given (GPU-trained) weights."""
+    from oracle import rdunet_ref as R
+    _, _, ev_noisy, ev_clean, _ = data
+    P = {k[5:]: v.detach().cpu().float() for k, v in state_dict.items() if k.startswith("unet.")}
+
+    def fn(x, tt):
+        return R.rdunet_t_forward(P, x, tt)
+
+    with torch.no_grad():
+        den = torch.cat([R.improved_sampling(fn, ev_noisy[i:i + args.eval_batch], args.timesteps)
+                         for i in range(0, ev_noisy.size(0), args.eval_batch)])
+    return psnr_per_image(den, ev_clean)
 
 
 def run_cpu(args, params, data):
@@ -173,6 +199,11 @@ def parser():
     ap.add_argument("--self-noise", action="store_true",
                     help="also train the CPU oracle from ~1e-6-perturbed weights: the protocol's noise floor")
     ap.add_argument("--keep-losses", action="store_true")
+    ap.add_argument("--part", choices=("all", "gpu", "cpu"), default="all",
+                    help="run only the GPU legs (on the MI355X box) or only the CPU-oracle legs (any host); "
+                         "--merge pairs the two files by seed")
+    ap.add_argument("--merge", nargs="+", default=None, metavar="JSON",
+                    help="combine --part gpu / --part cpu outputs (same config) and report")
     ap.add_argument("--out", default="")
     return ap
 
@@ -185,8 +216,18 @@ def _one(args, seed):
     params = make_params(R.param_shapes(a.base_filters), seed)
     data = make_data(a)
     r = {"seed": seed, "psnr_noisy_input": psnr_per_image(data[2], data[3])}
-    r["gpu_fp32"] = run_gpu(a, params, data, "fp32")
-    print(f"seed {seed}: gpu fp32 psnr {r['gpu_fp32']['psnr']:.4f}", flush=True)
+    gpu, cpu = args.part in ("all", "gpu"), args.part in ("all", "cpu")
+    if gpu:
+        r["gpu_fp32"] = run_gpu(a, params, data, "fp32")
+        print(f"seed {seed}: gpu fp32 psnr {r['gpu_fp32']['psnr']:.4f}", flush=True)
+        # inference parity at identical weights: the GPU-trained model, denoised by the oracle
+        r["oracle_eval_of_gpu_weights_psnr"] = oracle_eval_psnr(a, r["gpu_fp32"].pop("_state"), data)
+        r["delta_inference_db"] = r["gpu_fp32"]["psnr"] - r["oracle_eval_of_gpu_weights_psnr"]
+        if args.bf16:
+            r["gpu_bf16"] = run_gpu(a, params, data, "bf16")
+            r["gpu_bf16"].pop("_state")
+    if not cpu:
+        return r
     r["cpu_oracle_fp32"] = run_cpu(a, params, data)
     print(f"seed {seed}: cpu fp32 psnr {r['cpu_oracle_fp32']['psnr']:.4f}", flush=True)
     if args.self_noise:
@@ -195,8 +236,12 @@ def _one(args, seed):
         rng = np.random.default_rng(seed + 7)
         pert = {k: (v * (1 + 1e-6 * rng.standard_normal(v.shape))).astype(np.float32) for k, v in params.items()}
         r["cpu_oracle_fp32_perturbed"] = run_cpu(a, pert, data)
-    if args.bf16:
-        r["gpu_bf16"] = run_gpu(a, params, data, "bf16")
+    if not gpu:
+        return r
+    return _finish(args, r)
+
+
+def _finish(args, r):
     lg, lc = r["gpu_fp32"]["losses"], r["cpu_oracle_fp32"]["losses"]
     rel = [abs(x - y) / abs(y) for x, y in zip(lg, lc)]
     r["loss_traj_max_rel_diff"] = max(rel)
@@ -207,9 +252,49 @@ def _one(args, seed):
     return r
 
 
+def paired_stats(d):
+    """Mean, sd and two-sided 95 % Student-t interval of per-seed differences."""
+    n = len(d)
+    out = {"n": n, "per_seed_db": [float(x) for x in d], "mean_db": float(np.mean(d))}
+    if n > 1:
+        from scipy import stats
+        sd = float(np.std(d, ddof=1))
+        half = float(stats.t.ppf(0.975, n - 1)) * sd / math.sqrt(n)
+        out.update(sd_db=sd, ci95=[out["mean_db"] - half, out["mean_db"] + half], ci95_halfwidth_db=half)
+    return out
+
+
 def run(args):
     seeds = [args.seed + 100 * i for i in range(args.seeds)]
     runs = [_one(args, s) for s in seeds]
+    if args.part != "all":
+        return {"part": args.part, "config": {k: getattr(args, k) for k in (
+                    "steps", "batch", "size", "n_train", "n_eval", "base_filters", "timesteps", "sigma", "lr",
+                    "seed", "seeds")}, "runs": runs}
+    return summarize(args, runs)
+
+
+def merge(args):
+    """Pair --part gpu and --part cpu outputs by seed (configs must agree)."""
+    parts = [json.load(open(f)) for f in args.merge]
+    cfg = {k: v for k, v in parts[0]["config"].items() if k not in ("seed", "seeds")}
+    by_seed = {}
+    for prt in parts:
+        if {k: v for k, v in prt["config"].items() if k not in ("seed", "seeds")} != cfg:
+            raise SystemExit("configs differ")
+        for r in prt["runs"]:
+            by_seed.setdefault(r["seed"], {}).update(r)
+    runs = [r for _, r in sorted(by_seed.items()) if "gpu_fp32" in r and "cpu_oracle_fp32" in r]
+    for k, v in cfg.items():
+        setattr(args, k, v)
+    args.seed, args.seeds = runs[0]["seed"], len(runs)
+    args.self_noise = all("cpu_oracle_fp32_perturbed" in r for r in runs)
+    args.bf16 = all("gpu_bf16" in r for r in runs)
+    runs = [_finish(args, r) for r in runs]
+    return summarize(args, runs)
+
+
+def summarize(args, runs):
     mean = lambda leg: float(np.mean([r[leg]["psnr"] for r in runs]))
     res = {"protocol": "SURVEY.md §8d PSNR@sigma=25: identical init, data and t draws; Adam every step; "
                        "improved_sampling T=20 on a held-out set; hyperparams_search.py PSNR convention; "
@@ -219,20 +304,33 @@ def run(args):
            "psnr_noisy_input": float(np.mean([r["psnr_noisy_input"] for r in runs])),
            "psnr_gpu_fp32": mean("gpu_fp32"), "psnr_cpu_oracle_fp32": mean("cpu_oracle_fp32")}
     res["delta_db"] = res["psnr_gpu_fp32"] - res["psnr_cpu_oracle_fp32"]
+    d = np.array([r["gpu_fp32"]["psnr"] - r["cpu_oracle_fp32"]["psnr"] for r in runs])
+    res["paired"] = paired_stats(d)
     res["pass_0p05db"] = bool(abs(res["delta_db"]) <= 0.05)
+    res["ci95_within_0p05db"] = bool(res["paired"]["ci95"][0] >= -0.05 and res["paired"]["ci95"][1] <= 0.05) \
+        if len(d) > 1 else None
+    di = np.array([r["delta_inference_db"] for r in runs])
+    res["inference_parity"] = {"per_seed_db": [float(x) for x in di], "max_abs_db": float(np.max(np.abs(di)))}
     if args.self_noise:
         res["psnr_cpu_oracle_fp32_perturbed"] = mean("cpu_oracle_fp32_perturbed")
         res["self_noise_delta_db"] = res["psnr_cpu_oracle_fp32_perturbed"] - res["psnr_cpu_oracle_fp32"]
+    if args.self_noise:
+        res["self_noise_paired"] = paired_stats(np.array([r["cpu_oracle_fp32_perturbed"]["psnr"] -
+                                                          r["cpu_oracle_fp32"]["psnr"] for r in runs]))
     if args.bf16:
         res["psnr_gpu_bf16"] = mean("gpu_bf16")
         res["delta_bf16_vs_fp32_db"] = res["psnr_gpu_bf16"] - res["psnr_gpu_fp32"]
+        res["bf16_vs_oracle_paired"] = paired_stats(np.array([r["gpu_bf16"]["psnr"] - r["cpu_oracle_fp32"]["psnr"]
+                                                              for r in runs]))
     res["runs"] = runs
     return res
 
 
 def main():
     args = parser().parse_args()
-    res = run(args)
+    if args.part != "all":
+        args.keep_losses = True     # the merge compares the loss trajectories
+    res = merge(args) if args.merge else run(args)
     s = json.dumps(res, indent=1)
     print(s, flush=True)
     if args.out:

@@ -75,7 +75,8 @@ def test_backward_routing_plan():
     """Every gradient buffer is stored once before any accumulation, in
     backward execution order."""
     from vub_image_denoising_amd.engine import _assign_backward, _plan
-    layers, bufs = _plan(32, 3, True, 3)
+    prog = _plan(32, 3, True, 3)
+    layers, bufs = prog.layers, prog.bufs
     _assign_backward(layers)
     assert len(layers) == 69
     seen = set()
@@ -100,10 +101,35 @@ def test_cpu_tensors_fail_loudly():
         m(torch.zeros(1, 3, 16, 16), torch.zeros(1, 1, 1, 1))
 
 
-def test_blocks_refuse_standalone_forward():
+def test_block_forward_needs_gpu_tensors():
+    """A block's own forward runs on the GPU engine (no CPU path)."""
     import vub_image_denoising_amd as vm
-    with pytest.raises(RuntimeError):
+    with pytest.raises(RuntimeError, match="GPU"):
         vm.DenoisingBlock(32, 16, 32)(torch.zeros(1, 32, 8, 8))
+
+
+def test_block_programs():
+    """Every block of Unet_model.py:23-89 maps to an engine Program with the
+    reference's parameter names, input/output levels and channel counts."""
+    import vub_image_denoising_amd as vm
+    from vub_image_denoising_amd.engine import block_program
+    cases = [(vm.DenoisingBlock(32, 16, 32), [("X", 0, 32)], 0, 32, True, 4),
+             (vm.InputBlock(4, 32), [("X", 0, 4)], 0, 32, False, 2),
+             (vm.OutputBlock(32, 3), [("X", 0, 32)], 0, 3, False, 2),
+             (vm.DownsampleBlock(32, 64), [("X", 0, 32)], 1, 64, False, 1),
+             (vm.UpsampleBlock(64, 32, 32), [("U", 1, 64), ("CAT", 0, 32)], 0, 32, False, 2)]
+    for blk, inputs, olvl, oc, resid, nl in cases:
+        prog = block_program(blk)
+        assert prog.inputs == inputs and prog.out_level == olvl and prog.out_channels == oc
+        assert prog.resid_input == resid and len(prog.layers) == nl
+        names = {n for n, _ in blk.named_parameters()}
+        for L in prog.layers:
+            assert {L.name + ".weight", L.name + ".bias", L.act + ".weight"} <= names
+        assert prog.layers[-1].dst is None and all(L.dst is not None for L in prog.layers[:-1])
+    with pytest.raises(ValueError, match="multiples of 8"):
+        block_program(vm.DenoisingBlock(12, 6, 12))
+    with pytest.raises(ValueError, match="out_channels"):
+        block_program(vm.DenoisingBlock(32, 16, 48))
 
 
 def test_trainer_variants_keep_reference_signatures():

@@ -1,0 +1,207 @@
+"""The autograd boundary (engine._EngineFunction): the fused network and every
+block are autograd nodes whose inputs are the images AND the parameters, so the
+reference's training idioms behave as they do with aten ops — checked against
+the CPU oracle (oracle/rdunet_ref.py, which follows Unet_model.py:23-166).
+
+* ``torch.autograd.grad(loss, params)`` returns the gradients (no ``.grad``
+  writes) and equals ``loss.backward()``;
+* ``.grad`` of a fresh backward are views of one flat buffer (AccumulateGrad
+  adopts them), a second backward accumulates, gradients a caller still holds are
+  never overwritten;
+* two forwards of the same shape before one backward, ``retain_graph``, frozen
+  parameters and tensor hooks;
+* each block's own ``forward`` (Unet_model.py:23-89) against the oracle's block
+  functions, forward and backward, and the blocks composed one by one equal the
+  fused network.
+
+fp32 tolerances: forward rel-L2 <= 1e-5; gradients <= 1e-4 for a single block
+(a few layers of fp32 rounding) and <= 2e-3 for the whole 69-layer network (the
+budget of tests/test_gpu_fullsize.py)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from oracle import rdunet_ref as R  # noqa: E402
+
+
+def _rel(a, b):
+    a, b = a.detach().cpu().double(), b.detach().cpu().double()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def _net(F0=16, seed=0):
+    import vub_image_denoising_amd as vm
+    torch.manual_seed(seed)
+    return vm.RDUNet_T(base_filters=F0).cuda()
+
+
+def _data(B=2, S=32, seed=1):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.rand(B, 3, S, S, generator=g) * 2 - 1
+    t = torch.rand(B, 1, 1, 1, generator=g)
+    return x.cuda(), t.cuda()
+
+
+def _loss(m, x, t):
+    return m(x, t).square().mean()
+
+
+def test_autograd_grad_equals_backward_and_oracle():
+    m = _net()
+    x, t = _data()
+    params = list(m.parameters())
+    g = torch.autograd.grad(_loss(m, x, t), params)
+    assert all(p.grad is None for p in params)
+    _loss(m, x, t).backward()
+    for a, p in zip(g, params):
+        assert torch.equal(a, p.grad)
+    P = {n: p.detach().cpu().clone().requires_grad_(True) for n, p in m.named_parameters()}
+    rg = torch.autograd.grad(R.rdunet_t_forward(P, x.cpu(), t.cpu()).square().mean(), list(P.values()))
+    for (n, _), a, b in zip(m.named_parameters(), g, rg):
+        assert _rel(a, b) < 2e-3, (n, _rel(a, b))
+
+
+def test_grads_are_flat_views_and_accumulate():
+    from vub_image_denoising_amd.engine import find_flat
+    m = _net()
+    x, t = _data()
+    params = list(m.parameters())
+    _loss(m, x, t).backward()
+    fp = find_flat(params)
+    assert fp is not None   # AccumulateGrad adopted the flat views (no per-tensor copies)
+    g1 = fp.gflat.clone()
+    _loss(m, x, t).backward()           # lands in a second buffer, added into .grad
+    assert find_flat(params) is fp
+    assert torch.equal(fp.gflat, 2 * g1)
+    m.zero_grad(set_to_none=True)
+    _loss(m, x, t).backward()           # the first buffer is free again
+    assert find_flat(params) is fp and torch.equal(fp.gflat, g1)
+
+
+def test_held_gradients_are_not_overwritten():
+    m = _net()
+    params = list(m.parameters())
+    g1 = torch.autograd.grad(_loss(m, *_data(seed=1)), params)
+    keep = [g.clone() for g in g1]
+    g2 = torch.autograd.grad(_loss(m, *_data(seed=5)), params)
+    for a, b in zip(g1, keep):
+        assert torch.equal(a, b)
+    assert any(not torch.equal(a, b) for a, b in zip(g1, g2))
+
+
+def test_two_forwards_before_backward():
+    m = _net()
+    params = list(m.parameters())
+    (x1, t1), (x2, t2) = _data(seed=1), _data(seed=2)
+    ref1 = torch.autograd.grad(_loss(m, x1, t1), params)
+    ref2 = torch.autograd.grad(_loss(m, x2, t2), params)
+    l1, l2 = _loss(m, x1, t1), _loss(m, x2, t2)
+    g2 = torch.autograd.grad(l2, params)
+    g1 = torch.autograd.grad(l1, params)
+    for a, b in zip(g1, ref1):
+        assert torch.equal(a, b)
+    for a, b in zip(g2, ref2):
+        assert torch.equal(a, b)
+    (_loss(m, x1, t1) + _loss(m, x2, t2)).backward()
+    for p, a, b in zip(params, ref1, ref2):
+        assert torch.equal(p.grad, a + b)
+
+
+def test_retain_graph_and_release():
+    m = _net()
+    x, t = _data()
+    params = list(m.parameters())
+    y = m(x, t)
+    gy = torch.randn_like(y)
+    ref = torch.autograd.grad(y, params, gy)
+    y = m(x, t)
+    y.backward(gy, retain_graph=True)
+    y.backward(gy)
+    for p, r in zip(params, ref):
+        assert torch.equal(p.grad, 2 * r)
+    with pytest.raises(RuntimeError, match="released"):
+        y.backward(gy)                   # activations were released by the last backward
+
+
+def test_frozen_params_and_hooks():
+    m = _net()
+    x, t = _data()
+    for p in m.input_block.parameters():
+        p.requires_grad_(False)
+    seen = []
+    h = m.output_block.conv_2.weight.register_hook(lambda g: seen.append(g.clone()))
+    _loss(m, x, t).backward()
+    h.remove()
+    assert all(p.grad is None for p in m.input_block.parameters())
+    assert all(p.grad is not None for n, p in m.named_parameters() if not n.startswith("input_block"))
+    assert len(seen) == 1 and torch.equal(seen[0], m.output_block.conv_2.weight.grad)
+
+
+def test_input_gradient_vs_oracle():
+    m = _net()
+    x, t = _data()
+    xg = x.clone().requires_grad_(True)
+    (gx,) = torch.autograd.grad(_loss(m, xg, t), [xg])
+    P = {n: p.detach().cpu() for n, p in m.named_parameters()}
+    xr = x.cpu().requires_grad_(True)
+    (rx,) = torch.autograd.grad(R.rdunet_t_forward(P, xr, t.cpu()).square().mean(), [xr])
+    assert _rel(gx, rx) < 1e-4
+
+
+BLOCKS = [
+    ("DenoisingBlock", lambda vm: vm.DenoisingBlock(32, 16, 32), [(2, 32, 24, 40)],
+     lambda P, xs: R._dense_block(P, "", xs[0])),
+    ("InputBlock", lambda vm: vm.InputBlock(4, 32), [(2, 4, 24, 40)],
+     lambda P, xs: R._input_block(P, "", xs[0])),
+    ("OutputBlock", lambda vm: vm.OutputBlock(32, 3), [(2, 32, 24, 40)],
+     lambda P, xs: R._output_block(P, "", xs[0])),
+    ("DownsampleBlock", lambda vm: vm.DownsampleBlock(32, 64), [(2, 32, 24, 40)],
+     lambda P, xs: R._down(P, "", xs[0])),
+    ("UpsampleBlock", lambda vm: vm.UpsampleBlock(64, 32, 32), [(2, 64, 12, 20), (2, 32, 24, 40)],
+     lambda P, xs: R._up(P, "", xs[0], xs[1])),
+]
+
+
+@pytest.mark.parametrize("name,make,shapes,ref", BLOCKS, ids=[b[0] for b in BLOCKS])
+def test_block_forward_backward_vs_oracle(name, make, shapes, ref):
+    import vub_image_denoising_amd as vm
+    torch.manual_seed(3)
+    blk = make(vm)
+    P = {k: v.detach().clone().requires_grad_(True) for k, v in blk.state_dict().items()}
+    xs = [torch.randn(s) for s in shapes]
+    xr = [x.clone().requires_grad_(True) for x in xs]
+    yr = ref(P, xr)
+    gy = torch.randn_like(yr)
+    ref_g = torch.autograd.grad(yr, xr + list(P.values()), gy)
+    blk = blk.cuda()
+    xg = [x.cuda().requires_grad_(True) for x in xs]
+    y = blk(xg[0] if len(xg) == 1 else (xg[0], xg[1]))
+    assert y.shape == yr.shape and y.dtype == torch.float32
+    assert _rel(y, yr) < 1e-5, _rel(y, yr)
+    g = torch.autograd.grad(y, xg + list(blk.parameters()), gy.cuda())
+    names = [f"input{i}" for i in range(len(xg))] + [n for n, _ in blk.named_parameters()]
+    for n, a, b in zip(names, g, ref_g):
+        assert _rel(a, b) < 1e-4, (n, _rel(a, b))
+    with torch.no_grad():                # inference engine: same output
+        assert torch.equal(blk(xg[0] if len(xg) == 1 else (xg[0], xg[1])), y.detach())
+
+
+def test_blocks_compose_to_network():
+    """The reference's RDUNet_T.forward (Unet_model.py:138-166) spelled out with
+    the blocks' own forwards equals the fused network (and leaves it intact)."""
+    m = _net()
+    x, t = _data()
+    with torch.no_grad():
+        y = m(x, t)
+        xin = torch.cat([x, t.expand(x.size(0), 1, x.size(2), x.size(3))], 1)
+        o0 = m.block_0_1(m.block_0_0(m.input_block(xin)))
+        o1 = m.block_1_1(m.block_1_0(m.down_0(o0)))
+        o2 = m.block_2_1(m.block_2_0(m.down_1(o1)))
+        o3 = m.block_3_1(m.block_3_0(m.down_2(o2)))
+        o4 = m.block_2_3(m.block_2_2(m.up_2((o3, o2))))
+        o5 = m.block_1_3(m.block_1_2(m.up_1((o4, o1))))
+        o6 = m.block_0_3(m.block_0_2(m.up_0((o5, o0))))
+        yb = m.output_block(o6) + x
+        assert _rel(yb, y) < 1e-5
+        assert torch.equal(m(x, t), y)

@@ -8,16 +8,17 @@ order as the reference, so
 * ``torch.manual_seed(s); RDUNet_T(...)`` draws the same initial weights as the
   reference (same module construction order, same ``init_weights`` pass).
 
-The blocks are parameter containers.  ``RDUNet_T.forward`` runs the whole
-network as one fused launch sequence of hand-written gfx950 kernels
-(``engine.py`` → ``librdunet_hip.so``); there is no PyTorch-op or CPU path.
+``RDUNet_T.forward`` runs the whole network as one fused launch sequence of
+hand-written gfx950 kernels (``engine.py`` → ``librdunet_hip.so``); a block's
+own ``forward`` runs that block alone through the same engine and kernels.
+There is no PyTorch-op or CPU path.
 """
 from __future__ import annotations
 
 import torch
 import torch.nn as nn
 
-from .engine import run_unet
+from .engine import run_block, run_unet
 
 
 @torch.no_grad()
@@ -43,14 +44,33 @@ def init_weights(init_type='xavier'):
     return initializer
 
 
-class _FusedOnly:
-    def forward(self, *args, **kwargs):
-        raise RuntimeError(
-            f"{type(self).__name__} is executed as part of the fused RDUNet_T/RDUNet network on the GPU; "
-            "call the network's forward instead of the block's")
+_RUNTIME = ("_rdn_flat", "_rdn_packs", "_rdn_engines", "_rdn_prog")
 
 
-class DownsampleBlock(_FusedOnly, nn.Module):
+class _GpuBlock:
+    """A block's own forward: the block as a Program of the fused engine
+    (engine.block_program) — NCHW fp32 in/out, same kernels as inside the
+    network, autograd through inputs and parameters."""
+    compute_dtype = torch.float32
+
+    def set_compute_dtype(self, dtype):
+        dtype = {"fp32": torch.float32, "bf16": torch.bfloat16}.get(dtype, dtype)
+        if dtype not in (torch.float32, torch.bfloat16):
+            raise ValueError(f"compute dtype must be fp32 or bf16, got {dtype}")
+        self.compute_dtype = dtype
+        return self
+
+    def forward(self, x):
+        return run_block(self, [x])
+
+    def __getstate__(self):  # engines / packs are runtime state, not pickled
+        d = self.__dict__.copy()
+        for k in _RUNTIME:
+            d.pop(k, None)
+        return d
+
+
+class DownsampleBlock(_GpuBlock, nn.Module):
     """Unet_model.py:23-30: Conv2d(k=2, s=2) + PReLU."""
 
     def __init__(self, in_channels, out_channels):
@@ -59,7 +79,7 @@ class DownsampleBlock(_FusedOnly, nn.Module):
         self.actv = nn.PReLU(out_channels)
 
 
-class UpsampleBlock(_FusedOnly, nn.Module):
+class UpsampleBlock(_GpuBlock, nn.Module):
     """Unet_model.py:32-43: ConvTranspose2d(k=2, s=2) + PReLU, cat with the
     skip, Conv2d 3x3 + PReLU."""
 
@@ -70,8 +90,12 @@ class UpsampleBlock(_FusedOnly, nn.Module):
         self.actv = nn.PReLU(out_channels)
         self.actv_t = nn.PReLU(in_channels)
 
+    def forward(self, x):
+        upsample, concat = x
+        return run_block(self, [upsample, concat])
 
-class InputBlock(_FusedOnly, nn.Module):
+
+class InputBlock(_GpuBlock, nn.Module):
     """Unet_model.py:45-55: two Conv2d 3x3 + PReLU."""
 
     def __init__(self, in_channels, out_channels):
@@ -82,7 +106,7 @@ class InputBlock(_FusedOnly, nn.Module):
         self.actv_2 = nn.PReLU(out_channels)
 
 
-class OutputBlock(_FusedOnly, nn.Module):
+class OutputBlock(_GpuBlock, nn.Module):
     """Unet_model.py:57-67: Conv2d 3x3 + PReLU, Conv2d 3x3 + PReLU."""
 
     def __init__(self, in_channels, out_channels):
@@ -93,7 +117,7 @@ class OutputBlock(_FusedOnly, nn.Module):
         self.actv_2 = nn.PReLU(out_channels)
 
 
-class DenoisingBlock(_FusedOnly, nn.Module):
+class DenoisingBlock(_GpuBlock, nn.Module):
     """Unet_model.py:69-89: residual dense block (4 convs 3x3 + PReLU, dense
     concatenation, ``out_3 + x``)."""
 
@@ -164,7 +188,7 @@ class _RDUNetBase(nn.Module):
 
     def __getstate__(self):  # engines / flat buffers are runtime state, not pickled
         d = self.__dict__.copy()
-        for k in ("_rdn_flat", "_rdn_packs", "_rdn_engines"):
+        for k in _RUNTIME:
             d.pop(k, None)
         return d
 

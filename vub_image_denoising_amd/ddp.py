@@ -8,9 +8,12 @@ concatenated batch.
 
 Design for MI355X (xGMI point-to-point mesh):
 
-* the gradient lives in ONE flat fp32 buffer (``engine.FlatParams.gflat``),
-  laid out in module registration order (input block first), which is the
-  REVERSE of backward completion order;
+* a backward writes its gradients into ONE flat fp32 buffer
+  (``engine.ParamSet.grad_buffer``; ``.grad`` become views of it), laid out in
+  module registration order (input block first), which is the REVERSE of
+  backward completion order; that buffer is what is all-reduced (the engine
+  passes it to ``begin``), so with gradient accumulation only the new
+  contribution goes over the links, as with torch DDP;
 * it is cut into ~``bucket_mb`` buckets of contiguous parameter ranges; a bucket
   is launched (``all_reduce``, sum) on a side stream as soon as the engine's
   backward has finished the last layer whose gradients it holds, so RCCL rings
@@ -74,9 +77,13 @@ class GradSync:
         self._remaining = list(self.counts)
         self._launched = [False] * len(self.buckets)
         self._inv = None
+        self.buf = fp.gflat
 
     # --- engine hooks -------------------------------------------------
-    def begin(self):
+    def begin(self, buf=None):
+        """A backward starts producing its gradients into ``buf`` (a flat
+        buffer of ``fp``'s layout; default ``fp.gflat``)."""
+        self.buf = self.fp.gflat if buf is None else buf
         self._works = []
         self._remaining = list(self.counts)
         self._launched = [False] * len(self.buckets)
@@ -97,7 +104,7 @@ class GradSync:
             return
         self._launched[b] = True
         lo, hi = self.buckets[b]
-        view = self.fp.gflat[lo:hi]
+        view = self.buf[lo:hi]
         if self.overlap:
             self.stream.wait_stream(src if src is not None else torch.cuda.current_stream())
             with torch.cuda.stream(self.stream):
@@ -118,7 +125,7 @@ class GradSync:
             self._average()
 
     def _average(self):
-        g = self.fp.gflat
+        g = self.buf
         if g.is_cuda:
             from . import _hip as H
             if self._inv is None:

@@ -39,37 +39,104 @@ def _ru(x, m):
 
 
 # ----------------------------------------------------------------- parameters
-class FlatParams:
-    """Flat fp32 storage for a module's parameters (and gradients).
+_GPOOL_MAX = 4
 
-    The module's ``nn.Parameter`` objects keep their identity (optimizers and
-    ``state_dict`` see the usual tensors) but their ``.data`` become views of
-    ``self.flat``; ``.grad`` become views of ``self.gflat``."""
 
-    def __init__(self, module: torch.nn.Module, device):
+def _storage_refs(t: torch.Tensor) -> int:
+    """Tensors sharing ``t``'s storage (``t`` itself included)."""
+    return torch._C._storage_Use_Count(t.untyped_storage()._cdata) - 1
+
+
+class ParamSet:
+    """A module's parameters in a fixed order at aligned offsets of one flat fp32
+    index space, and the flat buffers their gradients are produced into.
+
+    The backward writes every weight gradient of one pass into ONE flat buffer
+    and hands autograd a fresh view per parameter: ``AccumulateGrad`` adopts a
+    view as ``p.grad`` when ``p.grad`` is None (the usual ``zero_grad()`` loop,
+    so ``.grad`` tensors are views of one flat buffer and clipping / the fused
+    optimizer / the DDP all-reduce stay single launches) and adds it into
+    ``p.grad`` otherwise, exactly as it does for aten's gradients;
+    ``torch.autograd.grad`` returns the views themselves.  A buffer is reused only
+    when no tensor references its storage any more (``p.grad`` views, grads a
+    caller kept), so a pass never overwrites a gradient anyone still holds."""
+
+    def _layout(self, module: torch.nn.Module, device):
         self.params = list(module.parameters())
         self.names = [n for n, _ in module.named_parameters()]
+        self.index = {n: i for i, n in enumerate(self.names)}
         offs, o = [], 0
         for p in self.params:
             offs.append(o)
             o = _ru(o + p.numel(), _ALIGN)
         self.numel = o
         self.offsets = offs
-        self.flat = torch.zeros(o, dtype=torch.float32, device=device)
-        self.gflat = torch.zeros(o, dtype=torch.float32, device=device)
-        self.views, self.gviews = [], []
+        self.device = device
+        self._shapes = [tuple(p.shape) for p in self.params]
+        self._strides = [torch.empty(s, device="meta").stride() for s in self._shapes]
+        self._gpool = [torch.zeros(o, dtype=torch.float32, device=device)]
+        self._gcur = self._gpool[0]
+        self._gexpect = {}
+        self.grad_sync = None   # ddp.GradSync attached by data-parallel training
+
+    @property
+    def gflat(self) -> torch.Tensor:
+        """The flat buffer the ``.grad`` tensors are views of (after
+        ``grads_are_views()``), else the last one a backward produced."""
+        return self._gcur
+
+    def grad_buffer(self) -> torch.Tensor:
+        """A flat gradient buffer nothing references (the caller zero-fills it)."""
+        for b in self._gpool:
+            if _storage_refs(b) == 1:
+                return b
+        b = torch.empty(self.numel, dtype=torch.float32, device=self.device)
+        if len(self._gpool) < _GPOOL_MAX:
+            self._gpool.append(b)
+        return b
+
+    def grad_views(self, buf: torch.Tensor, which=None) -> list:
+        """Fresh per-parameter views of a flat gradient buffer (None where
+        ``which[i]`` is false)."""
+        st = torch.as_strided
+        if which is None:
+            return [st(buf, s, r, o) for s, r, o in zip(self._shapes, self._strides, self.offsets)]
+        return [st(buf, s, r, o) if w else None for s, r, o, w in zip(self._shapes, self._strides, self.offsets, which)]
+
+    def grads_are_views(self) -> bool:
+        """Every ``p.grad`` is its view of one pooled flat buffer; that buffer
+        becomes ``gflat``."""
+        ptrs = [0 if p.grad is None else p.grad.data_ptr() for p in self.params]
+        for b in self._gpool:
+            exp = self._gexpect.get(b.data_ptr())
+            if exp is None:
+                base = b.data_ptr()
+                exp = self._gexpect[base] = [base + 4 * o for o in self.offsets]
+            if ptrs == exp:
+                self._gcur = b
+                return True
+        return False
+
+
+class FlatParams(ParamSet):
+    """Flat fp32 storage for a module's parameters (and gradients).
+
+    The module's ``nn.Parameter`` objects keep their identity (optimizers and
+    ``state_dict`` see the usual tensors) but their ``.data`` become views of
+    ``self.flat``; ``.grad`` become views of a flat gradient buffer (ParamSet)."""
+
+    def __init__(self, module: torch.nn.Module, device):
+        self._layout(module, device)
+        self.flat = torch.zeros(self.numel, dtype=torch.float32, device=device)
+        self.views = []
         with torch.no_grad():
-            for p, off in zip(self.params, offs):
+            for p, off in zip(self.params, self.offsets):
                 v = self.flat[off:off + p.numel()].view_as(p)
                 v.copy_(p.data.to(device=device, dtype=torch.float32))
                 p.data = v
                 self.views.append(v)
-                self.gviews.append(self.gflat[off:off + p.numel()].view_as(p))
-        self.device = device
         self._ptrs = [v.data_ptr() for v in self.views]
-        self._gptrs = [g.data_ptr() for g in self.gviews]
         self.generation = 0
-        self.grad_sync = None   # ddp.GradSync attached by data-parallel training
         _FLAT_REGISTRY[:] = [r for r in _FLAT_REGISTRY if r() is not None]
         _FLAT_REGISTRY.append(weakref.ref(self))
 
@@ -82,29 +149,28 @@ class FlatParams:
     def version_key(self):
         return (self.generation, sum(p._version for p in self.params))
 
-    def prepare_grads(self):
-        """Make every ``p.grad`` (of params that require grad) a view of
-        ``gflat`` holding its current accumulated value (0 if it was None)."""
-        if all(p.grad is None for p in self.params):
-            self.gflat.zero_()   # one memset (the common zero_grad(set_to_none=True) case)
-            for p, g in zip(self.params, self.gviews):
-                if p.requires_grad:
-                    p.grad = g
-            return
-        for p, g in zip(self.params, self.gviews):
-            cur = p.grad
-            if cur is None:
-                g.zero_()
-            elif cur.data_ptr() != g.data_ptr():
-                g.copy_(cur)
-            if p.requires_grad:
-                p.grad = g
 
-    def grads_are_views(self) -> bool:
-        grads = [p.grad for p in self.params]
-        if any(g is None for g in grads):
-            return False
-        return [g.data_ptr() for g in grads] == self._gptrs
+class BlockParams(ParamSet):
+    """The parameters of one block run on its own (``DenoisingBlock(...)(x)``):
+    used in place (no flat copy, so a block that is also part of a fused
+    network keeps sharing the network's storage); its GEMM packs are rebuilt
+    on every forward, as nothing tracks raw-pointer writes into that storage."""
+
+    def __init__(self, module: torch.nn.Module, device):
+        for n, p in module.named_parameters():
+            if p.device != device or p.dtype != torch.float32 or not p.is_contiguous():
+                raise RuntimeError(f"{type(module).__name__}: parameter {n} must be a contiguous fp32 tensor "
+                                   f"on {device} (got {p.dtype} on {p.device})")
+        self._layout(module, device)
+        self._ptrs = [p.data_ptr() for p in self.params]
+        self.generation = 0
+
+    def intact(self) -> bool:
+        return [p.data_ptr() for p in self.params] == self._ptrs
+
+    def version_key(self):
+        self.generation += 1
+        return self.generation
 
 
 _FLAT_REGISTRY: list = []
@@ -132,7 +198,8 @@ PLANE_PAD = int(os.environ.get("RDN_PLANE_PAD", "0"))
 
 def find_flat(params):
     """The FlatParams whose parameter list is exactly ``params`` (same objects,
-    same order) with every gradient one of its views, else None."""
+    same order) with every gradient its view of one flat gradient buffer
+    (which becomes its ``gflat``), else None."""
     params = list(params)
     for ref in _FLAT_REGISTRY:
         fp = ref()
@@ -151,6 +218,16 @@ def flat_params(module: torch.nn.Module, device) -> FlatParams:
         module._rdn_packs = {}
         module._rdn_engines = {}
     return fp
+
+
+def block_params(module: torch.nn.Module, device) -> BlockParams:
+    bp = getattr(module, "_rdn_flat", None)
+    if bp is None or bp.device != device or not bp.intact():
+        bp = BlockParams(module, device)
+        module._rdn_flat = bp
+        module._rdn_packs = {}
+        module._rdn_engines = {}
+    return bp
 
 
 # ----------------------------------------------------------------- layer plan
@@ -188,8 +265,33 @@ class ConvLayer:
     extra: dict = field(default_factory=dict)
 
 
-def _plan(F0: int, cin_img: int, has_t: bool, cout_img: int):
-    """Forward-ordered layer list + buffer shapes {name: (level, channels)}."""
+@dataclass
+class Program:
+    """What one engine runs: forward-ordered convs over named NHWC buffers
+    ``{name: (level, channels)}`` (level l = the input grid halved l times).
+
+    ``inputs`` are the NCHW fp32 tensors of forward, each stored at channel 0 of
+    its buffer ``(buffer, level, channels)``; ``image_input``: input 0 is the network's
+    image, packed into 8-channel rows by ``rdn_pack_input``, with the broadcast t
+    map as its next channel when ``time_input`` (RDUNet_T).  The last conv writes
+    the NCHW fp32 output of level ``out_level``, adding ``inputs[0]`` when
+    ``resid_input`` (the network's ``+ inputs``, Unet_model.py:166, or a dense
+    block's ``out_3 + x``, :89).  ``cb``: level -> plane width of the
+    channel-blocked buffers of that level (none: plain NHWC)."""
+    layers: list
+    bufs: dict
+    inputs: list
+    out_level: int
+    out_channels: int
+    resid_input: bool
+    time_input: bool = False
+    image_input: bool = False
+    cb: dict = field(default_factory=dict)
+    min_div: int = 1
+
+
+def _plan(F0: int, cin_img: int, has_t: bool, cout_img: int) -> Program:
+    """The whole network (Unet_model.py:92-166 / RDUNet_model.py)."""
     F = [F0 << l for l in range(4)]
     D = [f + 3 * (f // 2) for f in F]
     bufs = {"IN": (0, 8), "IB1": (0, F[0]), "O6": (0, F[0]), "OB1": (0, F[0]),
@@ -256,7 +358,70 @@ def _plan(F0: int, cin_img: int, has_t: bool, cout_img: int):
     c3("output_block.conv_1", "output_block.actv_1", 0, F[0], F[0], Slice("O6"), Slice("OB1"), 0)
     layers.append(ConvLayer("output_block.conv_2", "output_block.actv_2", "c3", 0, F[0], F[0], cout_img, 8,
                             Slice("OB1"), None, "PRE_OUT"))
-    return layers, bufs
+    return Program(layers, bufs, [("IN", 0, cin_img)], 0, cout_img, True, time_input=has_t, image_input=True,
+                   cb={l: F[l] // 2 for l in range(4)}, min_div=8)
+
+
+def block_program(block) -> Program:
+    """One block of Unet_model.py:23-89 on its own: NCHW fp32 in and out, the
+    same kernels and buffer conventions as inside the network.  Channel counts
+    on a conv's input side must be multiples of 8 (the NHWC K chunks); the
+    input block's image channels and the output block's image channels are
+    padded to 8."""
+    kind = type(block).__name__
+    bufs: dict = {}
+    layers: list[ConvLayer] = []
+
+    def need8(*cs):
+        for c in cs:
+            if c % 8:
+                raise ValueError(f"{kind}: the GPU kernels need channel counts that are multiples of 8; got {c}")
+
+    def c3(name, act, cin, cout, src, dst, cout_pad=None):
+        bufs[f"PRE_{name}"] = (0, cout_pad or cout)
+        layers.append(ConvLayer(name, act, "c3", 0, cin, _ru(cin, 8), cout, cout_pad or cout, src, dst,
+                                f"PRE_{name}"))
+
+    if kind == "DenoisingBlock":       # :69-89
+        C_, i, Co = block.conv_0.in_channels, block.conv_0.out_channels, block.conv_3.out_channels
+        if Co != C_:
+            raise ValueError(f"DenoisingBlock: out_3 + x needs out_channels == in_channels ({Co} != {C_})")
+        need8(C_, i)
+        bufs["X"] = (0, C_ + 3 * i)
+        for k in range(3):
+            c3(f"conv_{k}", f"actv_{k}", C_ + k * i, i, Slice("X"), Slice("X", C_ + k * i))
+        c3("conv_3", "actv_3", C_ + 3 * i, Co, Slice("X"), None)
+        return Program(layers, bufs, [("X", 0, C_)], 0, Co, True)
+    if kind == "InputBlock":           # :45-55
+        cin, F = block.conv_1.in_channels, block.conv_1.out_channels
+        need8(F)
+        bufs["X"], bufs["Y1"] = (0, _ru(cin, 8)), (0, F)
+        c3("conv_1", "actv_1", cin, F, Slice("X"), Slice("Y1"))
+        c3("conv_2", "actv_2", F, F, Slice("Y1"), None)
+        return Program(layers, bufs, [("X", 0, cin)], 0, F, False)
+    if kind == "OutputBlock":          # :57-67
+        F, co = block.conv_1.in_channels, block.conv_2.out_channels
+        need8(F)
+        bufs["X"], bufs["Y1"] = (0, F), (0, F)
+        c3("conv_1", "actv_1", F, F, Slice("X"), Slice("Y1"))
+        c3("conv_2", "actv_2", F, co, Slice("Y1"), None, cout_pad=_ru(co, 8))
+        return Program(layers, bufs, [("X", 0, F)], 0, co, False)
+    if kind == "DownsampleBlock":      # :23-30
+        cin, co = block.conv.in_channels, block.conv.out_channels
+        need8(cin, co)
+        bufs["X"], bufs["PRE_conv"] = (0, cin), (1, co)
+        layers.append(ConvLayer("conv", "actv", "down", 1, cin, cin, co, co, Slice("X"), None, "PRE_conv"))
+        return Program(layers, bufs, [("X", 0, cin)], 1, co, False, min_div=2)
+    if kind == "UpsampleBlock":        # :32-43, forward((upsample, concat))
+        cu, co = block.conv_t.in_channels, block.conv.out_channels
+        cc = block.conv.in_channels - cu
+        need8(cu, cc, co)
+        bufs["U"], bufs["CAT"], bufs["PRE_conv_t"] = (1, cu), (0, cc + cu), (0, cu)
+        layers.append(ConvLayer("conv_t", "actv_t", "up", 1, cu, cu, cu, cu, Slice("U"), Slice("CAT", cc),
+                                "PRE_conv_t"))
+        c3("conv", "actv", cc + cu, co, Slice("CAT"), None)
+        return Program(layers, bufs, [("U", 1, cu), ("CAT", 0, cc)], 0, co, False)
+    raise TypeError(f"no GPU program for {kind}")
 
 
 def _assign_backward(layers):
@@ -268,10 +433,6 @@ def _assign_backward(layers):
     for L in layers:
         L.ddst = None if L.dst is None else Slice("d" + L.dst.buf, L.dst.c0)
     for L in reversed(layers):
-        if L.name == "input_block.conv_1":
-            L.dsrc = Slice("dIN")
-            L.accum = False
-            continue
         L.dsrc = Slice("d" + L.src.buf, L.src.c0)
         L.accum = L.dsrc.buf in written
         written.add(L.dsrc.buf)
@@ -348,26 +509,27 @@ def weight_packs(module, fp, layers, dtype) -> WeightPacks:
 
 # ----------------------------------------------------------------- engine
 class UNetEngine:
-    """Buffers and prebuilt launch descriptors for one input shape."""
+    """Buffers and prebuilt launch descriptors of one Program (the network, or
+    one block) for one input shape (B, H, W of level 0)."""
 
-    def __init__(self, module, B, Hh, Ww, dtype, train: bool):
-        if Hh % 8 or Ww % 8:
-            raise RuntimeError(f"RDUNet needs H and W divisible by 8 (three 2x down-samplings); got {Hh}x{Ww}")
-        F0 = module.base_filters
-        if F0 % 16:
-            raise RuntimeError(f"base_filters must be a multiple of 16 for the NHWC/MFMA layout; got {F0}")
+    def __init__(self, module, B, Hh, Ww, dtype, train: bool, prog: Program | None = None, params=None):
+        if prog is None:
+            F0 = module.base_filters
+            if F0 % 16:
+                raise RuntimeError(f"base_filters must be a multiple of 16 for the NHWC/MFMA layout; got {F0}")
+            prog = _plan(F0, module.image_channels, module.time_conditioned, module.out_channels)
+        if Hh % prog.min_div or Ww % prog.min_div:
+            raise RuntimeError(f"{type(module).__name__} needs H and W divisible by {prog.min_div}; got {Hh}x{Ww}")
         self.module = module
+        self.prog = prog
         self.B, self.H, self.W = B, Hh, Ww
         self.dtype = dtype
         self.code = H.dtype_code(dtype)
         self.train = train
-        self.has_t = module.time_conditioned
-        self.cin_img = module.image_channels
-        self.cout_img = module.out_channels
         dev = next(module.parameters()).device
         self.device = dev
-        self.fp = flat_params(module, dev)
-        layers, bufspec = _plan(F0, self.cin_img, self.has_t, self.cout_img)
+        self.fp = params if params is not None else flat_params(module, dev)
+        layers, bufspec = prog.layers, prog.bufs
         _assign_backward(layers)
         self.layers = layers
         self.packs = weight_packs(module, self.fp, layers, dtype)
@@ -376,11 +538,15 @@ class UNetEngine:
         self.grid = [(B, Hh >> l, Ww >> l) for l in range(4)]
         self.bufs = {}
         self.geo = {}   # buffer name -> (pixel stride ps, plane stride pl); pl = 0: plain NHWC
-        F = [F0 << l for l in range(4)]
+        in_bufs = {b for b, _, _ in prog.inputs}
+        # buffers no layer writes in forward (pure inputs): their layers' input
+        # gradients are only computed when that input needs a gradient
+        self.pure_inputs = in_bufs - {L.dst.buf for L in layers if L.dst is not None}
 
         def alloc(name, lvl, ch):
-            cb = F[lvl] // 2
-            if PLANAR and name not in ("IN", "dIN") and not name.startswith("PRE_") and ch % cb == 0 and ch > cb:
+            cb = prog.cb.get(lvl, 0)
+            if (PLANAR and cb and name not in in_bufs and name[1:] not in in_bufs and not name.startswith("PRE_")
+                    and ch % cb == 0 and ch > cb):
                 pl = self.P[lvl] * cb + PLANE_PAD
                 t = torch.zeros(ch // cb, pl, dtype=dtype, device=dev)
                 self.geo[name] = (cb, pl)
@@ -412,7 +578,7 @@ class UNetEngine:
                                                                   L.cout_pad) for L in layers)
             self._build_bwd()
         self._build_info()
-        self.token = 0
+        self.lease = None   # weakref to the autograd graph's lease while it owns the activations
 
     # ------------------------------------------------------------------
     def _out_level(self, L):
@@ -460,7 +626,9 @@ class UNetEngine:
                 d.ncols, d.cout = 4 * L.cout, L.cout
                 flags |= H.EPI_SCATTER2
             if L.dst is None:
-                flags |= H.EPI_OUT_NCHW | H.EPI_RESID  # + inputs (Unet_model.py:166)
+                flags |= H.EPI_OUT_NCHW
+                if self.prog.resid_input:   # + inputs (Unet_model.py:166) / out_3 + x (:89)
+                    flags |= H.EPI_RESID
             else:
                 d.out, d.out_ps, d.out_c0, d.out_pl = self._slice(L.dst)
                 if L.resid is not None:
@@ -564,11 +732,10 @@ class UNetEngine:
                 part_need = max(part_need, splits * 2 * wg.mdim * 4)
             L.wgrad_desc = wg
             L.extra["wgrad"] = (splits, wg.mdim, wg.ndim, ndim_real, taps)
-            L.extra["grad_w"] = self.fp.gviews[self.fp.names.index(L.name + ".weight")]
-            L.extra["grad_b"] = self.fp.gviews[self.fp.names.index(L.name + ".bias")]
-            L.extra["grad_a"] = self.fp.gviews[self.fp.names.index(L.act + ".weight")]
+            pidx = [self.fp.index[n] for n in (L.name + ".weight", L.name + ".bias", L.act + ".weight")]
+            L.extra["pidx"] = pidx
+            L.extra["goff"] = [4 * self.fp.offsets[i] for i in pidx]   # byte offsets in a flat gradient buffer
             L.extra["olvl"] = olvl
-            L.extra["pidx"] = [self.fp.names.index(n) for n in (L.name + ".weight", L.name + ".bias", L.act + ".weight")]
         self.ws = torch.zeros(max(ws_need // 4, 4), dtype=torch.float32, device=self.device)
         pws = max(part_need, self.pws_bytes, 16) // 4
         self.pws = torch.zeros(self.slots, (pws + 3) // 4 * 4, dtype=torch.float32, device=self.device)
@@ -636,22 +803,41 @@ class UNetEngine:
             L.extra["info"] = info
 
     # ------------------------------------------------------------------
-    def forward(self, x: torch.Tensor, t: torch.Tensor | None) -> torch.Tensor:
+    def forward(self, xs, t: torch.Tensor | None = None) -> torch.Tensor:
+        """``xs``: the Program's NCHW fp32 inputs (contiguous, on the device)."""
         lib, st = H.lib(), H.stream_ptr()
-        B, Hh, Ww = self.B, self.H, self.W
+        prog = self.prog
+        if len(xs) != len(prog.inputs):
+            raise RuntimeError(f"expected {len(prog.inputs)} inputs, got {len(xs)}")
+        for (bname, lvl, ch), x in zip(prog.inputs, xs):
+            n, h, w = self.grid[lvl]
+            if tuple(x.shape) != (n, ch, h, w):
+                raise RuntimeError(f"input for {bname}: expected {(n, ch, h, w)}, got {tuple(x.shape)}")
         self.packs.refresh()
-        IN = self.bufs["IN"]
-        if self.has_t:
-            te = t.to(device=x.device, dtype=torch.float32).expand(B, 1, Hh, Ww)
-            H.check(lib.rdn_pack_input(self.code, x.data_ptr(), B, self.cin_img, Hh, Ww, te.data_ptr(),
-                                       te.stride(0), te.stride(2), te.stride(3), 1, IN.data_ptr(), 8, st),
-                    "pack_input")
+        x0 = xs[0]
+        if prog.image_input:
+            # network image input (+ the broadcast t map as channel cin_img), 8-channel rows
+            B, Hh, Ww = self.B, self.H, self.W
+            IN, cin = self.bufs["IN"], prog.inputs[0][2]
+            if prog.time_input:
+                te = t.to(device=x0.device, dtype=torch.float32).expand(B, 1, Hh, Ww)
+                rc = lib.rdn_pack_input(self.code, x0.data_ptr(), B, cin, Hh, Ww, te.data_ptr(), te.stride(0),
+                                        te.stride(2), te.stride(3), 1, IN.data_ptr(), 8, st)
+            else:
+                rc = lib.rdn_pack_input(self.code, x0.data_ptr(), B, cin, Hh, Ww, None, 0, 0, 0, 0,
+                                        IN.data_ptr(), 8, st)
+            H.check(rc, "pack_input")
         else:
-            H.check(lib.rdn_pack_input(self.code, x.data_ptr(), B, self.cin_img, Hh, Ww, None, 0, 0, 0, 0,
-                                       IN.data_ptr(), 8, st), "pack_input")
-        y = torch.empty(B, self.cout_img, Hh, Ww, dtype=torch.float32, device=x.device)
+            for (bname, lvl, ch), x in zip(prog.inputs, xs):
+                ptr, ps, c0, pl = self._slice(Slice(bname))
+                n, h, w = self.grid[lvl]
+                H.check(lib.rdn_nchw_to_nhwc(self.code, x.data_ptr(), n, ch, h, w, ptr, ps, c0, pl, 0, st),
+                        "nchw_to_nhwc")
+        n, h, w = self.grid[prog.out_level]
+        y = torch.empty(n, prog.out_channels, h, w, dtype=torch.float32, device=x0.device)
         last = self.layers[-1].fwd_desc
-        last.out_nchw, last.res_nchw = y.data_ptr(), x.data_ptr()
+        last.out_nchw = y.data_ptr()
+        last.res_nchw = x0.data_ptr() if prog.resid_input else None
         fwd = lib.rdn_conv_fwd
         tr = TRACER
         for L in self.layers:
@@ -661,32 +847,38 @@ class UNetEngine:
                 tr.stop(tok)
             if rc:
                 H.check(rc, f"conv_fwd[{L.name}]")
-        self.token += 1
         return y
 
-    def backward(self, dy: torch.Tensor, need_dx: bool):
-        """Reverse sweep.  Compute stream: PReLU backward (unfused layers) and the
-        dgrad chain.  Side stream (when enabled): each layer's wgrad + reduce, which
-        only wait for that layer's dYpre (event ``ev_ready``); a layer's unfused
-        PReLU backward waits for the side stream to release its ring slot (the
-        ``ev_done`` of the layer SLOTS earlier in backward order).  Gradient
-        buffers are never aliased (one per activation buffer) and a slice's
-        gradient is complete before its producer layer is reached, so the two
-        chains share nothing else but these slots."""
+    def backward(self, dy: torch.Tensor, need_dx):
+        """Reverse sweep; returns (input gradients (None where ``need_dx[i]`` is
+        false), the flat buffer holding every weight gradient of this pass).
+
+        Compute stream: PReLU backward (unfused layers) and the dgrad chain.  Side
+        stream (when enabled): each layer's wgrad + reduce, which only wait for
+        that layer's dYpre (event ``ev_ready``); a layer's unfused PReLU backward
+        waits for the side stream to release its ring slot (the ``ev_done`` of
+        the layer SLOTS earlier in backward order).  Gradient buffers are never
+        aliased (one per activation buffer) and a slice's gradient is complete
+        before its producer layer is reached, so the two chains share nothing
+        else but these slots."""
         if not self.train:
             raise RuntimeError("engine was built without saved activations (no_grad forward)")
         lib, st = H.lib(), H.stream_ptr()
-        self.fp.prepare_grads()
+        prog = self.prog
+        need_buf = {b: bool(nd) for (b, _, _), nd in zip(prog.inputs, need_dx)}
+        gbuf = self.fp.grad_buffer()
+        gbuf.zero_()
+        gbase = gbuf.data_ptr()
         sync = self.fp.grad_sync
         if sync is not None:
-            sync.begin()
+            sync.begin(gbuf)
         dy = dy.contiguous()
         side = None if SERIAL_BWD else self.side
         if side is not None:
             main = torch.cuda.current_stream()
             sst = side.cuda_stream
             self.ev_begin.record(main)
-            side.wait_event(self.ev_begin)   # gradients zeroed / accumulated state ready
+            side.wait_event(self.ev_begin)   # gradient buffer zeroed
         else:
             sst = st
         tr = TRACER
@@ -697,7 +889,6 @@ class UNetEngine:
             n, h, w = self.grid[olvl]
             P = self.P[olvl]
             pre = self.bufs[L.pre]
-            ga, gb = L.extra["grad_a"], L.extra["grad_b"]
             fused = L.extra["fused"]
             dyp, pws = L.extra["dyp"], L.extra["pws"]
             # unfused: the PReLU-backward pass leaves its dalpha/dbias partials in
@@ -720,7 +911,7 @@ class UNetEngine:
                 H.check(rc, f"prelu_bwd[{L.name}]")
             if side is not None:
                 L.extra["ev_ready"].record(main)
-            if L.name != "input_block.conv_1" or need_dx:
+            if L.src.buf not in self.pure_inputs or need_buf[L.src.buf]:
                 tok = tr.start(info["dgrad"]) if tr is not None else None
                 rc = lib.rdn_conv_fwd(C.byref(L.dgrad_desc), st)
                 if tok is not None:
@@ -737,9 +928,9 @@ class UNetEngine:
                 H.check(rc, f"wgrad[{L.name}]")
             splits, mdim, ndim, ndim_real, taps = L.extra["wgrad"]
             part_splits = 0 if fused else lib.rdn_prelu_bwd_blocks(self.code, P, L.cout_pad)
-            rc = lib.rdn_wgrad_reduce(self.ws.data_ptr(), splits, mdim, ndim, ndim_real, taps,
-                                      L.extra["grad_w"].data_ptr(), 1, pws, part_splits,
-                                      ga.data_ptr(), gb.data_ptr(), sst)
+            ow, ob, oa = L.extra["goff"]
+            rc = lib.rdn_wgrad_reduce(self.ws.data_ptr(), splits, mdim, ndim, ndim_real, taps, gbase + ow, 1, pws,
+                                      part_splits, gbase + oa, gbase + ob, sst)
             if rc:
                 H.check(rc, f"wgrad_reduce[{L.name}]")
             if side is not None:
@@ -751,31 +942,81 @@ class UNetEngine:
             main.wait_event(self.ev_end)
         if sync is not None:
             sync.finish()
-        if not need_dx:
-            return None
-        dx = dy.clone()  # global residual: output + inputs (Unet_model.py:166)
-        dIN = self.bufs["dIN"]
-        H.check(lib.rdn_nhwc_to_nchw(self.code, dIN.data_ptr(), dIN.shape[1], 0, 0, self.B, self.cin_img, self.H, self.W,
-                                     dx.data_ptr(), 1, st), "nhwc_to_nchw")
-        return dx
+        dxs = []
+        for i, ((bname, lvl, ch), nd) in enumerate(zip(prog.inputs, need_dx)):
+            if not nd:
+                dxs.append(None)
+                continue
+            n, h, w = self.grid[lvl]
+            if i == 0 and prog.resid_input:   # the residual's share: d(y)/d(input 0) = 1
+                dx, acc = dy.clone(), 1
+            else:
+                dx, acc = torch.empty(n, ch, h, w, dtype=torch.float32, device=dy.device), 0
+            ptr, ps, c0, pl = self._slice(Slice("d" + bname))
+            H.check(lib.rdn_nhwc_to_nchw(self.code, ptr, ps, c0, pl, n, ch, h, w, dx.data_ptr(), acc, st),
+                    "nhwc_to_nchw")
+            dxs.append(dx)
+        return dxs, gbuf
 
 
-class _UNetFunction(torch.autograd.Function):
+class _Lease:
+    """Held by one autograd graph while its engine's saved activations are its own."""
+    __slots__ = ("__weakref__",)
+
+
+def _engine_free(eng) -> bool:
+    return eng.lease is None or eng.lease() is None
+
+
+class _EngineFunction(torch.autograd.Function):
+    """One engine forward as one autograd node.  Inputs: the Program's input
+    tensors, then every parameter of the module, so ``torch.autograd.grad``,
+    ``requires_grad_(False)``, hooks and AccumulateGrad see the weights as the
+    reference's graph has them."""
+
     @staticmethod
-    def forward(ctx, engine, x, t, anchor):
-        y = engine.forward(x, t)
-        ctx.engine = engine
-        ctx.token = engine.token
-        return y
+    def forward(ctx, engine, lease, t, n_in, *tensors):
+        ctx.engine, ctx.lease, ctx.n_in = engine, lease, n_in
+        return engine.forward(tensors[:n_in], t)
 
     @staticmethod
     def backward(ctx, dy):
-        eng = ctx.engine
-        if eng.token != ctx.token:
-            raise RuntimeError("RDUNet engine activations were overwritten by a later forward of the same shape "
-                               "before this backward ran; call backward before the next forward")
-        dx = eng.backward(dy, ctx.needs_input_grad[1])
-        return None, dx, None, None
+        eng, n = ctx.engine, ctx.n_in
+        if eng.lease is None or eng.lease() is not ctx.lease:
+            raise RuntimeError("this graph's saved RDUNet activations were released by an earlier backward "
+                               "(use retain_graph=True to backward through it twice)")
+        needs = ctx.needs_input_grad
+        dxs, gbuf = eng.backward(dy, needs[4:4 + n])
+        if not torch._C._autograd._get_current_graph_task_keep_graph():
+            eng.lease = None          # activations free for the next forward
+        return (None, None, None, None, *dxs, *eng.fp.grad_views(gbuf, needs[4 + n:]))
+
+
+def _run(module, key_shape, xs, t, params, make_engine):
+    need_grad = torch.is_grad_enabled() and (any(x.requires_grad for x in xs) or
+                                             any(p.requires_grad for p in params.params))
+    key = key_shape + (module.compute_dtype, bool(need_grad))
+    pool = module._rdn_engines.setdefault(key, [])
+    if not need_grad:
+        if not pool:
+            pool.append(make_engine(False))
+        with torch.no_grad():
+            return pool[0].forward(xs, t)
+    # a graph owns its engine's activations until its backward (or until it is
+    # freed): a second forward before that backward gets a second engine
+    eng = next((e for e in pool if _engine_free(e)), None)
+    if eng is None:
+        eng = make_engine(True)
+        pool.append(eng)
+    lease = _Lease()
+    eng.lease = weakref.ref(lease)
+    return _EngineFunction.apply(eng, lease, t, len(xs), *xs, *params.params)
+
+
+def _f32_input(x, what):
+    if not isinstance(x, torch.Tensor) or x.dim() != 4:
+        raise RuntimeError(f"{what}: expected a [B,C,H,W] tensor")
+    return x.contiguous() if x.dtype == torch.float32 else x.float().contiguous()
 
 
 def run_unet(module, x: torch.Tensor, t: torch.Tensor | None) -> torch.Tensor:
@@ -785,19 +1026,23 @@ def run_unet(module, x: torch.Tensor, t: torch.Tensor | None) -> torch.Tensor:
         H.require_device(t)
     if x.dim() != 4 or x.size(1) != module.image_channels:
         raise RuntimeError(f"expected input [B,{module.image_channels},H,W], got {tuple(x.shape)}")
-    x = x.contiguous()
-    if x.dtype != torch.float32:
-        x = x.float()
-    need_grad = torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in module.parameters()))
-    dtype = module.compute_dtype
+    x = _f32_input(x, type(module).__name__)
     fp = flat_params(module, x.device)
-    key = (x.size(0), x.size(2), x.size(3), dtype, bool(need_grad))
-    eng = module._rdn_engines.get(key)
-    if eng is None:
-        eng = UNetEngine(module, x.size(0), x.size(2), x.size(3), dtype, bool(need_grad))
-        module._rdn_engines[key] = eng
-    if not need_grad:
-        with torch.no_grad():
-            return eng.forward(x, t)
-    anchor = fp.params[0]
-    return _UNetFunction.apply(eng, x, t, anchor)
+    B, Hh, Ww = x.size(0), x.size(2), x.size(3)
+    return _run(module, (B, Hh, Ww), [x], t, fp,
+                lambda train: UNetEngine(module, B, Hh, Ww, module.compute_dtype, train))
+
+
+def run_block(block, xs) -> torch.Tensor:
+    """Entry of the blocks' standalone ``forward`` (Unet_model.py:23-89)."""
+    xs = [_f32_input(x, type(block).__name__) for x in xs]
+    H.require_device(*xs, next(block.parameters()))
+    bp = block_params(block, xs[0].device)
+    prog = getattr(block, "_rdn_prog", None)
+    if prog is None:
+        prog = block._rdn_prog = block_program(block)
+    lvl0 = prog.inputs[0][1]
+    B, Hh, Ww = xs[0].size(0), xs[0].size(2) << lvl0, xs[0].size(3) << lvl0
+    return _run(block, (B, Hh, Ww), xs, None, bp,
+                lambda train: UNetEngine(block, B, Hh, Ww, block.compute_dtype, train,
+                                         prog=block_program(block), params=bp))

@@ -87,7 +87,7 @@ class FusedAdam(torch.optim.Optimizer):
         return loss
 
     def zero_grad(self, set_to_none: bool = True):
-        fp = self._fp or find_flat(self.param_groups[0]["params"])
+        fp = find_flat(self.param_groups[0]["params"])
         if fp is not None and not set_to_none:
             fp.gflat.zero_()
             return
