@@ -99,12 +99,13 @@ def extra_configs(dev, args):
     out = {}
     for key, batch, dtype, warm, steps in (("b32", 32, "bf16", 3, args.steps), ("fp32", 16, "fp32", 2, 6)):
         _log(f"extra config {key}: batch {batch} {dtype}")
-        tr = Trainer(dev, batch, args.size, args.base_filters, dtype)
+        tr = Trainer(dev, batch, args.size, args.base_filters, dtype, graph=args.graph == "on")
         for i in range(warm):
             tr.step(i)
         prof = tr.profile() if key == "b32" else None
         el, loss = tr.timed(steps)
-        r = {"per_gpu_batch": batch, "dtype": dtype, "steps": steps, "ms_per_step": round(el * 1e3 / steps, 3),
+        r = {"per_gpu_batch": batch, "dtype": dtype, "steps": steps, "graph": args.graph == "on",
+             "ms_per_step": round(el * 1e3 / steps, 3),
              "images_per_s": round(batch * steps / el, 2), "final_loss": round(loss.item(), 5)}
         if prof is not None:
             r["dense_conv_path"] = dense_conv_path(prof, batch)
@@ -302,7 +303,7 @@ class Trainer:
     """One RDUNet_T train step (the timed unit) for a (per-GPU batch, dtype):
     synthetic seeded data resident in HBM, FusedAdamW every step."""
 
-    def __init__(self, dev, batch, size, base_filters, dtype, rank=0, world=1):
+    def __init__(self, dev, batch, size, base_filters, dtype, rank=0, world=1, graph=False):
         import vub_image_denoising_amd as vm
         from vub_image_denoising_amd.ddp import GradSync
         from vub_image_denoising_amd.diffusion_RDUnet import DiffusionModel, train_step_device
@@ -321,18 +322,27 @@ class Trainer:
         torch.manual_seed(99 + rank)  # t draws (torch.randint on the device)
         self._train_step = train_step_device
         self.opt = None
+        self.graph = None
         self.step(0)  # builds the flat parameter buffer and the engine
         self.opt = FusedAdamW(self.model.parameters(), lr=1e-4, weight_decay=1e-4)
         if world > 1:
             self.unet._rdn_flat.grad_sync = GradSync(self.unet._rdn_flat, bucket_mb=25.0)
+        self.graph = None
+        if graph:   # the whole step as one hipGraph replay (train_graph.TrainStepGraph)
+            from vub_image_denoising_amd.train_graph import TrainStepGraph
+            self.graph = TrainStepGraph(self.model, self.opt, tuple(self.batches[0][0].shape), 'uniform', 1.0)
 
     def step(self, i):
         noisy, clean = self.batches[i % 3]
+        if self.graph is not None and not self.eager:
+            return self.graph(clean, noisy)
         opt = self.opt if self.opt is not None else self
         loss = self._train_step(self.model, clean, noisy, opt, "uniform", 1.0)
         if self.opt is not None:
             self.opt.step()
         return loss
+
+    eager = False   # profiling passes run the step eagerly (per-launch events)
 
     def zero_grad(self, set_to_none=True):   # stands in for the optimizer on the first step
         for p in self.model.parameters():
@@ -343,15 +353,18 @@ class Trainer:
         from vub_image_denoising_amd import engine as E
         prof = EventTracer()
         E.TRACER, E.SERIAL_BWD = prof, True
+        self.eager = True
         try:
             self.step(0)
         finally:
             E.TRACER, E.SERIAL_BWD = None, False
+            self.eager = False
         return prof
 
     def timed(self, steps, world=1, tracer=None):
         from vub_image_denoising_amd import engine as E
         E.TRACER = tracer
+        self.eager = tracer is not None
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -363,7 +376,19 @@ class Trainer:
             dist.barrier()
         el = time.perf_counter() - t0
         E.TRACER = None
+        self.eager = False
         return el, loss
+
+    def host_issue_ms(self, n=10):
+        """Host time to issue one step (median; the GPU drained before each)."""
+        ts = []
+        for i in range(n):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            self.step(i)
+            ts.append(time.perf_counter() - t0)
+        torch.cuda.synchronize()
+        return round(1e3 * sorted(ts)[n // 2], 3)
 
 
 DENSE_LEVELS = (0, 1)
@@ -406,6 +431,8 @@ def main():
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC passes (roofline.traffic)")
     ap.add_argument("--no-inference", action="store_true", help="skip the sampler measurements")
     ap.add_argument("--no-extra", action="store_true", help="skip the batch-32 and fp32 train-step lines")
+    ap.add_argument("--graph", choices=["on", "off"], default="on",
+                    help="time the step as one hipGraph replay (train_graph.TrainStepGraph) or eagerly")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
@@ -417,7 +444,8 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    tr = Trainer(dev, args.batch, args.size, args.base_filters, args.dtype, rank, world)
+    graph = args.graph == "on" and not args.pmc_child
+    tr = Trainer(dev, args.batch, args.size, args.base_filters, args.dtype, rank, world, graph=graph)
     for i in range(args.warmup):
         tr.step(i)
     torch.cuda.synchronize()
@@ -434,15 +462,26 @@ def main():
         with open(args.layer_report.replace(".json", "_per_layer.json"), "w") as f:
             json.dump(prof.per_layer(), f, indent=0)
 
-    # timed region: events only around the dominant kernel's launches
+    # timed region.  Eager: events around the dominant kernel's launches inside it.
+    # Graph: the replays are timed; the dominant kernel's launch times come from an
+    # eager pass of the same steps right after (events cannot be timed inside a replay)
     live = EventTracer(keys={dom})
-    el, loss = tr.timed(args.steps, world, live)
+    if graph:
+        el, loss = tr.timed(args.steps, world, None)
+        el_eager, _ = tr.timed(args.steps, world, live)
+    else:
+        el, loss = tr.timed(args.steps, world, live)
+        el_eager = el
     if world > 1:
-        tt = torch.tensor([el], device=dev)
+        tt = torch.tensor([el, el_eager], device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        el = tt.item()
+        el, el_eager = tt.tolist()
     loss_v = loss.item()
     d = live.summary()[dom]
+    host_ms = tr.host_issue_ms() if world == 1 else None
+    tr.eager = True
+    host_eager_ms = tr.host_issue_ms() if (world == 1 and graph) else host_ms
+    tr.eager = False
 
     if rank == 0:
         images = args.batch * world * args.steps
@@ -479,7 +518,7 @@ def main():
         roof["isolated_frac"] = round((flops_per / (iso_ms * 1e-3) / 1e12 / peak_mfma) if roof["bound"] == "mfma"
                                       else (bytes_per / (iso_ms * 1e-3) / 1e9 / PEAK_HBM_GBS), 4)
         roof["launches_per_step"] = d["n"] // args.steps
-        roof["share_of_step"] = round(d["ms"] / (el * 1e3), 4)
+        roof["share_of_step"] = round(d["ms"] / (el_eager * 1e3), 4)
         roof[f"dense_conv_path_b{args.batch}"] = dense_conv_path(prof, args.batch)
         extra = None
         if world == 1 and not (args.no_extra or args.pmc_child):
@@ -503,6 +542,10 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(el * 1e3 / args.steps, 3),
+            "execution": "hipGraph replay per step" if graph else "eager launches",
+            "eager_ms_per_step": round(el_eager * 1e3 / args.steps, 3),
+            "host_issue_ms_per_step": host_ms,
+            "eager_host_issue_ms_per_step": host_eager_ms,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,

@@ -205,3 +205,23 @@ def test_blocks_compose_to_network():
         yb = m.output_block(o6) + x
         assert _rel(yb, y) < 1e-5
         assert torch.equal(m(x, t), y)
+
+
+def test_untracked_weight_writes_need_mark_dirty():
+    """``p.data`` writes bypass torch's version counters; mark_weights_dirty()
+    makes the next forward repack (in-place ops on the parameter itself are seen)."""
+    import vub_image_denoising_amd as vm
+    m = _net()
+    x, t = _data()
+    with torch.no_grad():
+        y0 = m(x, t)
+        w = m.block_1_0.conv_2.weight
+        w.data.mul_(0.5)
+        m.mark_weights_dirty()
+        y1 = m(x, t)
+        fresh = vm.RDUNet_T(base_filters=16)
+        fresh.load_state_dict({k: v.cpu() for k, v in m.state_dict().items()})
+        assert torch.equal(fresh.cuda()(x, t), y1)
+        assert not torch.equal(y0, y1)
+        w.mul_(2.0)                      # tracked: no mark needed
+        assert torch.equal(m(x, t), y0)

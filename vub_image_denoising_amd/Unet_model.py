@@ -186,6 +186,16 @@ class _RDUNetBase(nn.Module):
         self.compute_dtype = dtype
         return self
 
+    def mark_weights_dirty(self):
+        """Parameters were written where torch's version counters do not see it
+        (``p.data.copy_(...)``, raw pointers): rebuild the GEMM weight packs on
+        the next forward.  Optimizer steps, ``load_state_dict`` and in-place ops
+        on the parameters themselves are tracked without this."""
+        fp = getattr(self, "_rdn_flat", None)
+        if fp is not None:
+            fp.generation += 1
+        return self
+
     def __getstate__(self):  # engines / flat buffers are runtime state, not pickled
         d = self.__dict__.copy()
         for k in _RUNTIME:

@@ -484,7 +484,6 @@ __global__ __launch_bounds__(NT, (BM * CK > 2560 ? 1 : 2)) void wgrad3_rows_kern
   };
 
   u32x4 dA[D_IT], gA[GD], hA[H_IT];
-#ifndef RDN_WROWS_PF2
   // one tile in flight: load t+1 during tile t's MFMAs
   if (t_beg < t_end) {
     load_tile(t_beg, dA, gA, hA);
@@ -500,33 +499,6 @@ __global__ __launch_bounds__(NT, (BM * CK > 2560 ? 1 : 2)) void wgrad3_rows_kern
       __syncthreads();
     }
   }
-#else
-  // two tiles in flight (register sets A/B): a tile's global loads have two tile
-  // computations to land instead of one.  Invariant at the loop top: LDS holds
-  // tile t, set A holds (loads of) tile t+1
-  u32x4 dB[D_IT], gB[GD], hB[H_IT];
-  if (t_beg < t_end) {
-    load_tile(t_beg, dA, gA, hA);
-    store_tile(dA, gA, hA);
-  }
-  if (t_beg + 1 < t_end) load_tile(t_beg + 1, dA, gA, hA);
-  __syncthreads();
-  for (int t = t_beg; t < t_end; t += 2) {
-    if (t + 2 < t_end) load_tile(t + 2, dB, gB, hB);
-    compute_tile();
-    __syncthreads();
-    if (t + 1 >= t_end) break;
-    store_tile(dA, gA, hA);
-    __syncthreads();
-    if (t + 3 < t_end) load_tile(t + 3, dA, gA, hA);
-    compute_tile();
-    __syncthreads();
-    if (t + 2 < t_end) {
-      store_tile(dB, gB, hB);
-      __syncthreads();
-    }
-  }
-#endif
 
   if constexpr (GATE) {
     if (do_part) {
@@ -585,20 +557,9 @@ Plan plan(const rdn_wgrad_desc* d) {
 #ifndef RDN_NO_WROWS
   if (d->dtype == RDN_BF16) {
     // rows kernel: the widest channel group whose accumulators fit (BM x 9 CK per block)
-    // accumulator budget BM x CK (RDN_WROWS_MAXACC): <= 2560 keeps 2 blocks per CU,
-    // up to 4096 runs one block per CU with the wider channel group
-    static const int maxacc = [] {
-      const char* e = getenv("RDN_WROWS_MAXACC");
-      const int v = e ? atoi(e) : 2560;
-      return v < 2560 ? 2560 : v > 4096 ? 4096 : v;
-    }();
-    // RDN_WROWS_BM=128: 128 output channels per block for mdim >= 128 (dY tile read
-    // once per column group for twice the channels)
-    static const bool bm128 = [] {
-      const char* e = getenv("RDN_WROWS_BM");
-      return e && atoi(e) == 128;
-    }();
-    const int bm = bm128 && d->mdim >= 128 && maxacc >= 4096 ? 128 : p.bm;
+    // accumulator budget BM x CK <= 2560: two blocks per CU (measured r01: a
+    // 4096 budget at one block per CU, and 128-channel blocks, were slower)
+    const int maxacc = 2560, bm = p.bm;
     static const int cands[] = {96, 80, 64, 48, 32, 16, 8};
     for (int c : cands)
       if (d->ndim % c == 0 && c * bm <= maxacc) { p.ck = c; p.rows = 1; p.bm = bm; break; }
@@ -692,7 +653,6 @@ int rdn_wgrad3_launch(const rdn_wgrad_desc* d, hipStream_t st) {
   if (p.rows) {
     if (p.bm == 16) return launch_rows_ck<16>(d, p, st);
     if (p.bm == 32) return launch_rows_ck<32>(d, p, st);
-    if (p.bm == 128) return launch_rows_ck<128>(d, p, st);
     return launch_rows_ck<64>(d, p, st);
   }
   if (d->dtype == RDN_BF16) {

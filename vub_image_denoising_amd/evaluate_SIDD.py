@@ -100,9 +100,10 @@ def main(noisy_mat_file="evaluate_SIDD/ValidationNoisyBlocksSrgb.mat",
     dataloader = DataLoader(Subset(dataset, indices), batch_size=batch_size, shuffle=False, num_workers=4)
     device = torch.device("cuda")
     model = DiffusionModel(RDUNet_T(base_filters=base_filters), timesteps=timesteps).to(device)
-    if os.path.exists(checkpoint_path):
-        ckpt = torch.load(checkpoint_path, map_location=device, weights_only=True)
-        model.load_state_dict(ckpt["model_state_dict"])
+    if not os.path.exists(checkpoint_path):   # the reference's torch.load raises too
+        raise FileNotFoundError(f"checkpoint not found: {checkpoint_path}")
+    ckpt = torch.load(checkpoint_path, map_location=device, weights_only=True)
+    model.load_state_dict(ckpt["model_state_dict"])
     avg_psnr, avg_ssim, avg_time, samples = evaluate_model(model, dataloader, device)
     print(f"Average PSNR: {avg_psnr:.2f}")
     print(f"Average SSIM: {avg_ssim:.4f}")

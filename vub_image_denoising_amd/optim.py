@@ -28,6 +28,7 @@ class FusedAdam(torch.optim.Optimizer):
         self.grad_scale = grad_scale
         self._fp = None
         self._step = 0
+        self._step_dev = None   # device step counter (use_device_step)
 
     def _bind(self):
         params = self.param_groups[0]["params"]
@@ -55,8 +56,28 @@ class FusedAdam(torch.optim.Optimizer):
                 raise RuntimeError(f"FusedAdam: parameters were saved at different step counts {sorted(steps)}")
             self._step = steps.pop() if steps else 0
             self._steps.fill_(self._step)
+            if self._step_dev is not None:
+                if self._step_dev.device == fp.device:
+                    self._step_dev.fill_(self._step)
+                else:
+                    self._step_dev = torch.full((), self._step, dtype=torch.int64, device=fp.device)
             self._views()
         return fp
+
+    def use_device_step(self):
+        """Keep the step count in device memory, incremented and read by the
+        update kernels, so a hipGraph-captured step stays exact on every replay
+        (train_graph.TrainStepGraph); the host count mirrors it."""
+        fp = self._bind()
+        if self._step_dev is None:
+            self._step_dev = torch.full((), self._step, dtype=torch.int64, device=fp.device)
+        return self
+
+    def _replayed(self):
+        """A captured step ran (host mirror of the device step count)."""
+        self._step += 1
+        self._steps.fill_(self._step)
+        self._fp.generation += 1
 
     def _views(self):
         fp = self._fp
@@ -79,10 +100,15 @@ class FusedAdam(torch.optim.Optimizer):
         self._step += 1
         self._steps.fill_(self._step)
         b1, b2 = g["betas"]
-        H.check(H.lib().rdn_adam_step(fp.flat.data_ptr(), fp.gflat.data_ptr(), self._m.data_ptr(), self._v.data_ptr(),
-                                      fp.numel, float(g["lr"]), float(b1), float(b2), float(g["eps"]),
-                                      float(g["weight_decay"]), 1 if self.decoupled else 0, self._step, None,
-                                      float(self.grad_scale), H.stream_ptr()), "adam_step")
+        lib, st = H.lib(), H.stream_ptr()
+        sd = None
+        if self._step_dev is not None:
+            H.check(lib.rdn_counter_inc(self._step_dev.data_ptr(), st), "counter_inc")
+            sd = self._step_dev.data_ptr()
+        H.check(lib.rdn_adam_step(fp.flat.data_ptr(), fp.gflat.data_ptr(), self._m.data_ptr(), self._v.data_ptr(),
+                                  fp.numel, float(g["lr"]), float(b1), float(b2), float(g["eps"]),
+                                  float(g["weight_decay"]), 1 if self.decoupled else 0, self._step, sd,
+                                  float(self.grad_scale), st), "adam_step")
         fp.generation += 1  # weights changed behind torch's version counters: repack
         return loss
 

@@ -1,0 +1,134 @@
+"""hipGraph capture of one whole train step: the t draw, the interpolation, the
+fused RDUNet_T forward, the Charbonnier loss, the backward, clip_grad_norm_ and
+the fused Adam(W) update (diffusion_RDUnet.py:76-115 + ``optimizer.step()``),
+replayed with ONE host launch per step instead of ~700 kernel launches issued
+from Python.
+
+What makes the step capturable:
+
+* every buffer the step touches exists before capture (engine activations and
+  launch descriptors, the flat gradient buffer, clip and Adam workspaces):
+  warm-up steps build them, then their effect on the weights, the Adam moments,
+  the step count and the RNG is rolled back, so the first replay IS the model's
+  next step;
+* the Adam step count lives in device memory (FusedAdam.use_device_step), so
+  bias corrections advance on every replay;
+* ``torch.randint`` t draws use torch's graph-safe Philox generator (every
+  replay advances its offset exactly as an eager step does); the 'biased'
+  distribution draws on the CPU in the reference (:71-73), so its t are drawn
+  on the host per call and copied into the graph's t input;
+* values baked into the graph — lr, betas, eps, weight decay, clip value,
+  compute dtype — are compared on every call; a change (an LR scheduler step)
+  re-captures.
+
+The graph owns the parameters' ``.grad`` (views of the flat gradient buffer its
+backward writes); an eager step in between is allowed and does not disturb it.
+"""
+from __future__ import annotations
+
+import torch
+
+from .diffusion_RDUnet import sample_biased, train_step_device
+from .engine import find_flat
+from .optim import FusedAdam
+
+
+def _node_count(g):
+    """Kernel/memset/copy nodes of a captured graph (None if not exposed)."""
+    try:
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so")
+        raw = g.raw_cuda_graph()
+        n = ctypes.c_size_t(0)
+        if hip.hipGraphGetNodes(ctypes.c_void_p(raw), None, ctypes.byref(n)) != 0:
+            return None
+        return n.value
+    except Exception:
+        return None
+
+
+class TrainStepGraph:
+    def __init__(self, model, optimizer, shape, distribution_choice='uniform', clip_value=1.0, t_input=False,
+                 warmup=2):
+        if not isinstance(optimizer, FusedAdam):
+            raise TypeError("TrainStepGraph needs the fused optimizer (optim.FusedAdam / FusedAdamW)")
+        self.model, self.opt = model, optimizer
+        self.dist, self.clip = distribution_choice, clip_value
+        dev = next(model.parameters()).device
+        self.dev = dev
+        self.clean = torch.zeros(shape, dtype=torch.float32, device=dev)
+        self.noisy = torch.zeros(shape, dtype=torch.float32, device=dev)
+        self.host_t = distribution_choice == 'biased'
+        self.t = torch.zeros(shape[0], dtype=torch.float32, device=dev) if (t_input or self.host_t) else None
+        self.graph = None
+        self._build(warmup)
+
+    # ------------------------------------------------------------------
+    def _hyper(self):
+        g = self.opt.param_groups[0]
+        return (float(g["lr"]), tuple(g["betas"]), float(g["eps"]), float(g["weight_decay"]), float(self.clip),
+                float(self.opt.grad_scale), self.model.unet.compute_dtype)
+
+    def _body(self):
+        loss = train_step_device(self.model, self.clean, self.noisy, self.opt, self.dist, self.clip, t=self.t)
+        self.opt.step()
+        return loss
+
+    def _build(self, warmup):
+        rng = torch.cuda.get_rng_state(self.dev)
+        params = list(self.model.parameters())
+        side = torch.cuda.Stream(device=self.dev)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            if find_flat(params) is None or self.opt._fp is None:
+                # gradients as flat views, so the optimizer can bind (no update yet)
+                train_step_device(self.model, self.clean, self.noisy, self.opt, self.dist, self.clip, t=self.t)
+            self.opt.use_device_step()
+            fp, opt = self.opt._fp, self.opt
+            snap = (fp.flat.clone(), opt._m.clone(), opt._v.clone(), opt._step)
+            for _ in range(max(1, warmup)):
+                self._body()
+            fp.flat.copy_(snap[0])
+            opt._m.copy_(snap[1])
+            opt._v.copy_(snap[2])
+            opt._step = snap[3]
+            opt._steps.fill_(opt._step)
+            opt._step_dev.fill_(opt._step)
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize(self.dev)
+        fp.generation += 1
+        for wp in self.model.unet._rdn_packs.values():
+            wp.key = None          # the weight repack is the graph's first launch
+        self.graph = None
+        g = torch.cuda.CUDAGraph(keep_graph=True)
+        with torch.cuda.graph(g):
+            self.loss = self._body().detach()
+        self.graph_nodes = _node_count(g)
+        g.instantiate()
+        self.graph = g
+        self._captured = self._hyper()
+        # capture ran nothing: undo its host-side effects (step count, pack keys)
+        opt._step = snap[3]
+        opt._steps.fill_(opt._step)
+        fp.generation += 1
+        torch.cuda.set_rng_state(rng, self.dev)
+
+    # ------------------------------------------------------------------
+    def __call__(self, clean_images, noisy_images, t=None):
+        """One train step on this batch; returns the loss (a device tensor, valid
+        until the next call)."""
+        if self._hyper() != self._captured:
+            self._build(1)
+        self.clean.copy_(clean_images)
+        self.noisy.copy_(noisy_images)
+        if self.t is not None:
+            if t is None:
+                if not self.host_t:
+                    raise ValueError("this graph was built with t_input=True: pass t")
+                t = sample_biased(self.clean.size(0), self.model.timesteps)
+            self.t.copy_(t)
+        elif t is not None:
+            raise ValueError("this graph draws t itself (build it with t_input=True to pass t)")
+        self.graph.replay()
+        self.opt._replayed()
+        return self.loss
