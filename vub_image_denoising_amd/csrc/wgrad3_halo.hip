@@ -544,7 +544,7 @@ __global__ __launch_bounds__(NT, (BM * CK > 2560 ? 1 : 2)) void wgrad3_rows_kern
   }
 }
 
-struct Plan { int bm, ck, rows, mtiles, chunks, tiles_x, tiles_y, ntiles, tpb, splits; };
+struct Plan { int bm, ck, rows, glds, mtiles, chunks, tiles_x, tiles_y, ntiles, tpb, splits, chunks_rows; };
 
 Plan plan(const rdn_wgrad_desc* d) {
   Plan p;
@@ -565,11 +565,28 @@ Plan plan(const rdn_wgrad_desc* d) {
       if (d->ndim % c == 0 && c * bm <= maxacc) { p.ck = c; p.rows = 1; p.bm = bm; break; }
   }
 #endif
-  p.mtiles = (d->mdim + p.bm - 1) / p.bm;
-  p.chunks = d->ndim / p.ck;
+  p.chunks_rows = d->ndim / p.ck;   // the PReLU-gate fusion decision (rdn_wgrad_chunks) is made on these
+  p.glds = 0;
   p.tiles_x = (d->w + TW - 1) / TW;
   p.tiles_y = (d->h + TH - 1) / TH;
   p.ntiles = d->n * p.tiles_x * p.tiles_y;
+  // multi-chunk launches without the gate: the LDS-DMA pipelined kernel
+  // (wgrad3_glds.hip), one block per CU
+  if (p.rows && p.chunks_rows > 1 && rdn_wgrad3_glds_pick(d, &p.bm, &p.ck)) {
+    p.glds = 1;
+    p.mtiles = (d->mdim + p.bm - 1) / p.bm;
+    p.chunks = d->ndim / p.ck;
+    const int base = p.mtiles * p.chunks;
+    int s = d->splits > 0 ? d->splits : 256 / base;
+    const int maxs = (p.ntiles + 1) / 2;                             // >= 2 tiles per block
+    if (s > maxs) s = maxs;
+    if (s < 1) s = 1;
+    p.tpb = (p.ntiles + s - 1) / s;
+    p.splits = s;
+    return p;
+  }
+  p.mtiles = (d->mdim + p.bm - 1) / p.bm;
+  p.chunks = d->ndim / p.ck;
   const int base = p.mtiles * p.chunks;
   // blocks per launch (RDN_WGRAD_BLOCKS): one per CU.  The weight gradients run on
   // the side stream beside the dgrad chain, where fewer, longer blocks (and half
@@ -645,11 +662,14 @@ int launch_ck(const rdn_wgrad_desc* d, const Plan& p, hipStream_t st) {
 }  // namespace
 
 int rdn_wgrad3_splits(const rdn_wgrad_desc* d) { return plan(d).splits; }
-int rdn_wgrad3_chunks(const rdn_wgrad_desc* d) { return plan(d).chunks; }
+int rdn_wgrad3_chunks(const rdn_wgrad_desc* d) { return plan(d).chunks_rows; }
 
 int rdn_wgrad3_launch(const rdn_wgrad_desc* d, hipStream_t st) {
   const Plan p = plan(d);
   if (p.ck <= 0) { rdn_set_error("rdn_conv_wgrad(conv3): ndim=%d", d->ndim); return RDN_E_SHAPE; }
+  if (p.glds)
+    return rdn_wgrad3_glds_launch(d, p.bm, p.ck, p.mtiles * p.chunks * p.splits, p.tiles_x, p.tiles_y, p.ntiles,
+                                  p.tpb, st);
   if (p.rows) {
     if (p.bm == 16) return launch_rows_ck<16>(d, p, st);
     if (p.bm == 32) return launch_rows_ck<32>(d, p, st);
