@@ -103,10 +103,11 @@ int rdn_conv3_launch(const rdn_conv_desc* d, hipStream_t st);
 int rdn_conv3_chunk_impl(int cin, int dtype);
 int rdn_conv3_chunk_pow2(int cin, int cap);
 int rdn_conv3_ws_launch(const rdn_conv_desc* d, int ck, hipStream_t st);
+int rdn_conv3_wsd_launch(const rdn_conv_desc* d, int ck, hipStream_t st);
 int rdn_wgrad3_launch(const rdn_wgrad_desc* d, hipStream_t st);
 int rdn_wgrad3_splits(const rdn_wgrad_desc* d);
 int rdn_wgrad3_chunks(const rdn_wgrad_desc* d);
-int rdn_wgrad3_glds_pick(const rdn_wgrad_desc* d, int* bm, int* ck);
+int rdn_wgrad3_glds_pick(const rdn_wgrad_desc* d, int single_chunk, int* bm, int* ck);
 int rdn_wgrad3_glds_launch(const rdn_wgrad_desc* d, int bm, int ck, int blocks, int tiles_x, int tiles_y, int ntiles,
                            int tpb, hipStream_t st);
 

@@ -12,25 +12,30 @@
 // every tile goes straight to LDS with global_load_lds_dwordx4 (no VGPR staging)
 // into a ring of NS = 3 LDS stages: while tile t is multiplied, tiles t+1 and t+2
 // are in flight.  Each wave waits only for its own DMAs with a counted
-// `s_waitcnt vmcnt(G)` and a raw s_barrier publishes them (an LDS-DMA is a
-// pending write on the VM counter, so __syncthreads() would drain the whole ring:
+// `s_waitcnt vmcnt` and a raw s_barrier publishes them (an LDS-DMA is a pending
+// write on the VM counter, so __syncthreads() would drain the whole ring:
 // cdna_hip_programming.md §5 "Pipelining across barriers").  The barrier also
 // retires the reads of the stage the next DMA overwrites (it was read one tile
 // earlier).
 //
+// GATE (the level-0/1 single-chunk layers): the saved PReLU input arrives by DMA
+// beside dY and one pass over the LDS tile turns dY into dYpre in place (aten's
+// PReLU backward), accumulating the dalpha / dbias partials of the block's
+// channels in registers; they are written per split like rdn_prelu_bwd's.
+//
 // LDS images.  One DMA wave-instruction writes 1 KiB contiguously (lane l ->
 // bytes l*16..l*16+15), so the images are dense rows (dY: BM*2 bytes per pixel;
 // halo: CK*2 bytes per pixel) and bank conflicts of the ds_read_b64_tr_b16
-// fragment reads are removed by an XOR swizzle of the 16-byte units applied on the
-// per-lane SOURCE address:  unit' = unit ^ 2*s(x),  s(x) = (x / (256/RB)) mod
-// (RB/32), where x is the pixel's column inside its tile row (0..15) or halo row
-// (0..17).  A half-wave's transpose read touches 8 consecutive columns of one row
-// x one 32-byte unit pair; rows that share banks (x and x + 256/RB, ...) get
-// distinct unit pairs.  Because s depends on the column only, every fragment
-// address is a per-lane base fixed for the launch plus an immediate.
+// fragment reads are removed by rotating each row's 16-byte units by rot(x),
+// x = the pixel's column in its tile row (0..15) or halo row (0..17), applied on
+// the per-lane SOURCE address (rotations from an exhaustive check of the read
+// patterns: conflict-free for every row size used).  Because the rotation depends
+// on the column only, every fragment address is a per-lane base fixed for the
+// launch plus an immediate.
 //
-// Pixels outside the image (partial tiles, halo borders) load 16 zero bytes from
-// a device-side zero block, so stale stage bytes never reach the MFMAs.
+// Pixels outside the image (partial tiles, halo borders) and channels past mdim
+// load 16 zero bytes from a device-side zero block, so stale stage bytes never
+// reach the MFMAs.
 #include "rdn_common.h"
 
 #include <cstdlib>
@@ -42,38 +47,63 @@ __device__ __attribute__((aligned(64))) unsigned int g_wglds_zero[16];
 
 constexpr int TH = 8, TW = 16, TP = TH * TW;
 constexpr int HW_ = TW + 2, HP = (TH + 2) * HW_;
+constexpr int LDS_MAX = 160 * 1024;
 
-template <int BM, int CK>
+template <int BM, int CK, bool GATE>
 struct Geo {
   static constexpr int NW = 4, NTH = 256;                // waves per block (one per SIMD)
-  static constexpr int NCOL = 9 * CK, NT_ALL = NCOL / 16;
-  // waves as WMv (along M) x WNv (along the 9*CK columns) with the same number of
-  // n-tiles for every wave (a wave-dependent trip count costs accumulator copies)
-  static constexpr int WNv = NT_ALL % 4 == 0 ? 4 : 2, WMv = NW / WNv;
-  static constexpr int NTW = NT_ALL / WNv;                // n-tiles per wave
+  static constexpr int NCOL = 9 * CK, NT_ALL = (NCOL + 15) / 16;
+  // waves as WMv (along M) x WNv (along the 9*CK columns), the same number of
+  // n-tiles for every wave (a wave-dependent trip count costs accumulator copies);
+  // n-tiles past NT_ALL are computed on a valid column and not stored
+  static constexpr int WNv = (BM == 64 && NT_ALL % 4 != 0) ? 2 : 4, WMv = NW / WNv;
+  static constexpr int NTW = (NT_ALL + WNv - 1) / WNv;    // n-tiles per wave
   static constexpr int MTW = BM / 16 / WMv;               // 16-row m-tiles per wave
-  static constexpr int RA = BM * 2, RB = CK * 2;         // bytes per dY / halo pixel row
+  static constexpr int RA = BM * 2, RB = CK * 2;          // bytes per dY / halo pixel row
+  static constexpr int UA = RA / 16, UB = RB / 16;        // 16-B units per row
   static constexpr int A_PIECES = TP * RA / 1024;
-  static constexpr int PA = A_PIECES / NW;               // dY pieces per wave and tile
-  static constexpr int PB = ((HP * RB + 1023) / 1024 + NW - 1) / NW;
-  static constexpr int B_PIECES = PB * NW;               // last ones partly padding (zero source)
-  static constexpr int STAGE = (A_PIECES + B_PIECES) * 1024;
-  static constexpr int G = PA + PB;                      // DMAs per wave and tile (vmcnt unit)
-  static_assert(NT_ALL % WNv == 0 && MTW >= 1 && BM % (16 * WMv) == 0, "wave grid");
-  static_assert(A_PIECES % NW == 0, "dY pieces split evenly over the waves");
-  static_assert(CK % 16 == 0 && RB <= 256 && RA <= 256 && RA >= 64 && RB >= 64, "image geometry");
+  static constexpr int PA = A_PIECES / NW;                // dY (and PReLU-input) pieces per wave and tile
+  static constexpr int HPC = (HP * RB + 1023) / 1024;     // halo pieces (wave w: w, w+4, ...)
+  static constexpr int HPW = (HPC + NW - 1) / NW;
+  static constexpr int B_OFF = (GATE ? 2 : 1) * A_PIECES * 1024;
+  static constexpr int STAGE = B_OFF + HPC * 1024;
+  static constexpr int NS = 3 * STAGE <= LDS_MAX ? 3 : 2;
+  static constexpr bool OK = NS * STAGE <= LDS_MAX && MTW >= 1;
+  static_assert(A_PIECES % NW == 0 && CK % 8 == 0, "image geometry");
 };
 
-template <int RB>
-__device__ __forceinline__ int swz(int x) { return ((x / (256 / RB)) % (RB / 32)) * 2; }
+// unit rotation of a RBYTES-byte image row at column x (bank-conflict-free
+// ds_read_b64_tr_b16 of 8 consecutive columns x one 32-byte unit pair)
+template <int RBYTES>
+__device__ __forceinline__ int rot(int x) {
+  constexpr int U = RBYTES / 16;
+  if constexpr (RBYTES == 64) return (x >> 1) % U;
+  else if constexpr (RBYTES == 128) return x % U;
+  else if constexpr (RBYTES == 192) return ((x >> 2) * 6) % U;
+  else if constexpr (RBYTES == 256) return x % U;
+  else return 0;                                          // 32, 96, 160: conflict-free as is
+}
 
 template <int N>
 __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+__device__ __forceinline__ void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// DMAs wave w issues per tile: PA_ dY (+ PReLU-input) pieces + halo pieces w, w+4, ... < HPC
+template <int PA_, int HPC>
+__device__ __forceinline__ void wait_own(int wave, bool one_ahead) {
+  if (!one_ahead) { wait_vm<0>(); return; }
+  switch (wave) {
+    case 0: wait_vm<PA_ + (HPC + 3) / 4>(); break;
+    case 1: wait_vm<PA_ + (HPC + 2) / 4>(); break;
+    case 2: wait_vm<PA_ + (HPC + 1) / 4>(); break;
+    default: wait_vm<PA_ + HPC / 4>(); break;
+  }
+}
 
 // One LDS-DMA wave-instruction: 16 B per lane from `src` to LDS byte dst + lane*16
 // (dst wave-uniform, in M0).  Inline asm, so that the compiler does not see an
 // LDS write pending on the VM counter: with the builtin it waits vmcnt(0) before
-// every ds_read of the array, which drains the ring (the counted waits below are
+// every ds_read of the array, which drains the ring (the counted waits above are
 // the only ordering, cdna_hip_programming.md §5, "Read a staged buffer one phase
 // AFTER the wait that retires it").
 __device__ __forceinline__ void glds16(const void* src, unsigned dst) {
@@ -87,11 +117,13 @@ __device__ __forceinline__ unsigned lds_addr(const unsigned char* p) {
   return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) unsigned char*)p;
 }
 
-template <int BM, int CK, int NS>
-__global__ __launch_bounds__(256, 1) void wgrad3_glds_kernel(rdn_wgrad_desc d, int tiles_x, int tiles_y,
-                                                                          int ntiles, int tiles_per_block) {
-  using G_ = Geo<BM, CK>;
-  constexpr int RA = G_::RA, RB = G_::RB, NW = G_::NW, MTW = G_::MTW, NTW = G_::NTW;
+template <int BM, int CK, bool GATE>
+__global__ __launch_bounds__(256, 1) void wgrad3_glds_kernel(rdn_wgrad_desc d, int tiles_x, int tiles_y, int ntiles,
+                                                             int tiles_per_block) {
+  using G_ = Geo<BM, CK, GATE>;
+  constexpr int RA = G_::RA, RB = G_::RB, UA = G_::UA, UB = G_::UB, NW = G_::NW, MTW = G_::MTW, NTW = G_::NTW;
+  constexpr int NS = G_::NS, PA = G_::PA, HPC = G_::HPC, HPW = G_::HPW;
+  constexpr int VEC = 8;
   __shared__ __attribute__((aligned(1024))) unsigned char lds[NS * G_::STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -105,34 +137,37 @@ __global__ __launch_bounds__(256, 1) void wgrad3_glds_kernel(rdn_wgrad_desc d, i
   const int t_cnt = max(0, min(t_beg + tiles_per_block, ntiles) - t_beg);
   const int H = d.h, W = d.w;
   const bf16* __restrict__ A = (const bf16*)d.a;
+  const bf16* __restrict__ Gt = (const bf16*)d.a_gate;
   const bf16* __restrict__ Bx = (const bf16*)d.b;
   const bf16* const zero = (const bf16*)g_wglds_zero;
 
   // ---- per-lane DMA source geometry (tile-invariant)
-  int a_rel[G_::PA], a_py[G_::PA], a_px[G_::PA];
-  bool a_ok[G_::PA];
+  int a_rel[PA], g_rel[GATE ? PA : 1], a_py[PA], a_px[PA];
+  bool a_ok[PA];
 #pragma unroll
-  for (int j = 0; j < G_::PA; ++j) {
+  for (int j = 0; j < PA; ++j) {
     const int off = (wave + NW * j) * 1024 + lane * 16;
     const int r = off / RA, px = r % TW;
-    const int u = ((off % RA) >> 4) ^ swz<RA>(px);
-    const int m = m0 + u * 8;
+    const int u = ((off % RA) / 16 - rot<RA>(px) + UA) % UA;   // logical unit of this physical slot
+    const int m = m0 + u * VEC;
     a_ok[j] = m < d.mdim;
     a_py[j] = r / TW;
     a_px[j] = px;
     a_rel[j] = (a_py[j] * W + px) * (int)d.a_ps + rdn_coff32(d.a_c0 + (a_ok[j] ? m : 0), (int)d.a_ps, (int)d.a_pl);
+    if constexpr (GATE)
+      g_rel[j] = (a_py[j] * W + px) * (int)d.a_gate_ps + rdn_coff32(a_ok[j] ? m : 0, (int)d.a_gate_ps, (int)d.a_gate_pl);
   }
-  int b_rel[G_::PB], b_hy[G_::PB], b_hx[G_::PB];
-  bool b_ok[G_::PB];
+  int b_rel[HPW], b_hy[HPW], b_hx[HPW];
+  bool b_ok[HPW];
 #pragma unroll
-  for (int j = 0; j < G_::PB; ++j) {
+  for (int j = 0; j < HPW; ++j) {
     const int off = (wave + NW * j) * 1024 + lane * 16;
     const int hr = off / RB, hx = hr % HW_;
-    const int u = ((off % RB) >> 4) ^ swz<RB>(hx);
+    const int u = ((off % RB) / 16 - rot<RB>(hx) + UB) % UB;
     b_ok[j] = hr < HP;
     b_hy[j] = hr / HW_;
     b_hx[j] = hx;
-    b_rel[j] = (b_hy[j] * W + hx) * (int)d.b_ps + rdn_coff32(d.b_c0 + c0 + u * 8, (int)d.b_ps, (int)d.b_pl);
+    b_rel[j] = (b_hy[j] * W + hx) * (int)d.b_ps + rdn_coff32(d.b_c0 + c0 + u * VEC, (int)d.b_ps, (int)d.b_pl);
   }
 
   auto issue = [&](int t, int stage) {
@@ -143,18 +178,56 @@ __global__ __launch_bounds__(256, 1) void wgrad3_glds_kernel(rdn_wgrad_desc d, i
     const bool full = y0 + TH <= H && x0 + TW <= W;
     const bool interior = y0 >= 1 && y0 + TH + 1 <= H && x0 >= 1 && x0 + TW + 1 <= W;
     const bf16* const ab = A + pix0 * d.a_ps;
+    const bf16* const gb = GATE ? Gt + pix0 * d.a_gate_ps : nullptr;
     const bf16* const hb = Bx + (pix0 - W - 1) * d.b_ps;   // halo pixel (0, 0) = image (y0 - 1, x0 - 1)
-    const unsigned st = __builtin_amdgcn_readfirstlane(lds_addr(lds) + stage * G_::STAGE);
+    const unsigned st = lds_addr(lds) + stage * G_::STAGE;
 #pragma unroll
-    for (int j = 0; j < G_::PA; ++j) {
+    for (int j = 0; j < PA; ++j) {
       const bool ok = a_ok[j] & (full | ((y0 + a_py[j] < H) & (x0 + a_px[j] < W)));
       glds16(ok ? (const void*)(ab + a_rel[j]) : (const void*)zero, st + (wave + NW * j) * 1024);
+      if constexpr (GATE)
+        glds16(ok ? (const void*)(gb + g_rel[j]) : (const void*)zero, st + (G_::A_PIECES + wave + NW * j) * 1024);
     }
 #pragma unroll
-    for (int j = 0; j < G_::PB; ++j) {
+    for (int j = 0; j < HPW; ++j) {
+      if (wave + NW * j >= HPC) break;   // wave-uniform
       const bool ok = b_ok[j] & (interior | (((unsigned)(y0 - 1 + b_hy[j]) < (unsigned)H) &
                                              ((unsigned)(x0 - 1 + b_hx[j]) < (unsigned)W)));
-      glds16(ok ? (const void*)(hb + b_rel[j]) : (const void*)zero, st + (G_::A_PIECES + wave + NW * j) * 1024);
+      glds16(ok ? (const void*)(hb + b_rel[j]) : (const void*)zero, st + G_::B_OFF + (wave + NW * j) * 1024);
+    }
+  };
+
+  // ---- PReLU-backward gate (GATE): thread = one logical 16-B channel unit of
+  // pixel rows tid/UA, tid/UA + 256/UA, ...; its 8 channels are fixed for the launch
+  constexpr int GROWS = 256 / UA;                          // rows per pass
+  const int gu = tid % UA;
+  float galpha[GATE ? VEC : 1], sa[GATE ? VEC : 1], sb[GATE ? VEC : 1];
+  const bool do_part = GATE && d.part != nullptr && by == 0;
+  if constexpr (GATE) {
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+      const int m = m0 + gu * VEC + k;
+      galpha[k] = m < d.mdim ? d.a_gate_alpha[m] : 0.f;
+      sa[k] = 0.f;
+      sb[k] = 0.f;
+    }
+  }
+  auto gate_pass = [&](int stage) {
+    unsigned char* const st = lds + stage * G_::STAGE;
+#pragma unroll
+    for (int pr = tid / UA; pr < TP; pr += GROWS) {
+      const int off = pr * RA + ((gu + rot<RA>(pr % TW)) % UA) * 16;
+      float dy[VEC], x[VEC];
+      Unit16<bf16>::unpack(*(const u32x4*)(st + off), dy);
+      Unit16<bf16>::unpack(*(const u32x4*)(st + G_::A_PIECES * 1024 + off), x);
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) {
+        const bool pos = x[k] > 0.f;
+        if (!pos) sa[k] += x[k] * dy[k];
+        dy[k] = pos ? dy[k] : galpha[k] * dy[k];
+        sb[k] += dy[k];   // dbias sums dYpre before its rounding, as rdn_prelu_bwd does
+      }
+      *(u32x4*)(st + off) = Unit16<bf16>::pack(dy);
     }
   };
 
@@ -163,16 +236,17 @@ __global__ __launch_bounds__(256, 1) void wgrad3_glds_kernel(rdn_wgrad_desc d, i
   int aoff[MTW];
 #pragma unroll
   for (int i = 0; i < MTW; ++i)
-    aoff[i] = xa * RA + (((wm * (BM / G_::WMv) / 8 + 2 * i + (pp >> 1)) ^ swz<RA>(xa)) << 4) + (pp & 1) * 8;
+    aoff[i] = xa * RA + (((wm * (BM / G_::WMv) / 8 + 2 * i + (pp >> 1)) + rot<RA>(xa)) % UA) * 16 + (pp & 1) * 8;
   int boff[NTW];
 #pragma unroll
   for (int j = 0; j < NTW; ++j) {
     const int nt = wn + G_::WNv * j;
-    const int c = nt * 16 + 4 * pp;
+    int c = nt * 16 + 4 * pp;
+    c = c < G_::NCOL ? c : 0;                             // padded columns: a valid read, never stored
     const int tp = c / CK, ci = c - tp * CK;
     const int ky = tp / 3, kx = tp - 3 * ky;
     const int hx = xa + kx;
-    boff[j] = G_::A_PIECES * 1024 + (ky * HW_ + hx) * RB + (((ci >> 3) ^ swz<RB>(hx)) << 4) + (ci & 7) * 2;
+    boff[j] = G_::B_OFF + (ky * HW_ + hx) * RB + (((ci >> 3) + rot<RB>(hx)) % UB) * 16 + (ci & 7) * 2;
   }
 
   f32x4 acc[MTW][NTW];
@@ -183,46 +257,91 @@ __global__ __launch_bounds__(256, 1) void wgrad3_glds_kernel(rdn_wgrad_desc d, i
 
   auto compute = [&](int stage) {
     const unsigned char* const st = lds + stage * G_::STAGE;
-#pragma unroll
-    for (int ks = 0; ks < TP / 32; ++ks) {
-      bf16x8 af[MTW];
+    // all fragments of k-step ks+1 are read before the MFMAs of ks: one wave per
+    // SIMD, so nothing else hides the LDS latency
+    bf16x8 af[2][MTW], bfr[2][NTW];
+    auto ld = [&](int ks, int buf) {
 #pragma unroll
       for (int i = 0; i < MTW; ++i) {
         const unsigned char* a = st + aoff[i] + ks * 32 * RA;
         const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, a));
         const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, a + 16 * RA));
-        af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        af[buf][i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
       }
 #pragma unroll
       for (int j = 0; j < NTW; ++j) {
         const unsigned char* b = st + boff[j] + ks * 2 * HW_ * RB;
         const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, b));
         const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, b + HW_ * RB));
-        const bf16x8 bfr = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-#pragma unroll
-        for (int i = 0; i < MTW; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, acc[i][j], 0, 0, 0);
+        bfr[buf][j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
       }
+    };
+    ld(0, 0);
+#pragma unroll
+    for (int ks = 0; ks < TP / 32; ++ks) {
+      if (ks + 1 < TP / 32) ld(ks + 1, (ks + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < NTW; ++j)
+#pragma unroll
+        for (int i = 0; i < MTW; ++i)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks & 1][i], bfr[ks & 1][j], acc[i][j], 0, 0, 0);
     }
   };
 
-  // ---- NS-deep ring: tiles it+1, it+2 in flight while tile it is multiplied;
+  // ---- NS-deep ring: up to NS-1 tiles in flight while tile it is multiplied;
   // unrolled by NS so that every stage offset is a constant
-  static_assert(NS == 3, "wait counts below assume a 3-stage ring");
-  if (t_cnt > 0) issue(t_beg, 0);
-  if (t_cnt > 1) issue(t_beg + 1, 1);
+  constexpr int PA_ALL = PA * (GATE ? 2 : 1);
+  for (int k = 0; k < NS - 1; ++k)
+    if (k < t_cnt) issue(t_beg + k, k);
   auto step = [&](int it, auto S) {
     constexpr int s = decltype(S)::value;
-    if (it + 1 < t_cnt) wait_vm<G_::G>();   // own DMAs of tile it landed (tile it+1 may still fly)
-    else wait_vm<0>();
+    // own DMAs of tile it landed (with NS = 3 tile it+1 may still fly)
+    wait_own<PA_ALL, HPC>(wave, NS == 3 && it + 1 < t_cnt);
     __builtin_amdgcn_s_barrier();           // everyone's landed; everyone done reading tile it-1's stage
     asm volatile("" ::: "memory");
-    if (it + 2 < t_cnt) issue(t_beg + it + 2, (s + 2) % NS);
+    if (it + NS - 1 < t_cnt) issue(t_beg + it + NS - 1, (s + NS - 1) % NS);
+    if constexpr (GATE) {
+      gate_pass(s);
+      wait_lgkm0();
+      __builtin_amdgcn_s_barrier();         // gated dY visible to every wave
+      asm volatile("" ::: "memory");
+    }
     compute(s);
   };
   for (int it = 0; it < t_cnt; it += NS) {
     step(it, std::integral_constant<int, 0>{});
-    if (it + 1 < t_cnt) step(it + 1, std::integral_constant<int, 1>{});
-    if (it + 2 < t_cnt) step(it + 2, std::integral_constant<int, 2>{});
+    if (it + 1 < t_cnt) step(it + 1, std::integral_constant<int, 1 % NS>{});
+    if constexpr (NS == 3)
+      if (it + 2 < t_cnt) step(it + 2, std::integral_constant<int, 2 % NS>{});
+  }
+
+  if constexpr (GATE) {
+    if (do_part) {
+      // per-block channel partials -> part[split][0|1][m] (LDS reduce, fixed order)
+      wait_vm<0>();
+      __syncthreads();   // every wave done with the ring
+      float* red = (float*)lds;
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) {
+        red[tid * VEC + k] = sa[k];
+        red[256 * VEC + tid * VEC + k] = sb[k];
+      }
+      __syncthreads();
+      if (tid < BM) {
+        const int cg = tid / VEC, k = tid % VEC;
+        float a = 0.f, b = 0.f;
+        for (int r = 0; r < GROWS; ++r) {
+          a += red[(r * UA + cg) * VEC + k];
+          b += red[256 * VEC + (r * UA + cg) * VEC + k];
+        }
+        const int m = m0 + tid;
+        if (m < d.mdim) {
+          d.part[((int64_t)bz * 2 + 0) * d.mdim + m] = a;
+          d.part[((int64_t)bz * 2 + 1) * d.mdim + m] = b;
+        }
+      }
+    }
   }
 
   // D[m][n]: row = g*4 + e (output channel), col = li (tile column)
@@ -232,6 +351,7 @@ __global__ __launch_bounds__(256, 1) void wgrad3_glds_kernel(rdn_wgrad_desc d, i
   for (int j = 0; j < NTW; ++j) {
     const int nt = wn + G_::WNv * j;
     const int c = nt * 16 + li;
+    if (nt >= G_::NT_ALL || c >= G_::NCOL) continue;
     const int tp = c / CK, ci = c - tp * CK;
     const int col = tp * d.ndim + c0 + ci;
 #pragma unroll
@@ -246,21 +366,64 @@ __global__ __launch_bounds__(256, 1) void wgrad3_glds_kernel(rdn_wgrad_desc d, i
 
 template <int BM, int CK>
 int launch(const rdn_wgrad_desc* d, int blocks, int tiles_x, int tiles_y, int ntiles, int tpb, hipStream_t st) {
-  RDN_PROBE("wgrad3_glds_kernel<bf16,%d,%d>", BM, CK);
-  wgrad3_glds_kernel<BM, CK, 3><<<blocks, 256, 0, st>>>(*d, tiles_x, tiles_y, ntiles, tpb);
-  return rdn_check_launch("rdn_conv_wgrad(conv3 glds)");
+  if (d->a_gate) {
+    if constexpr (Geo<BM, CK, true>::OK) {
+      RDN_PROBE("wgrad3_glds_kernel<bf16,%d,%d,gate>", BM, CK);
+      wgrad3_glds_kernel<BM, CK, true><<<blocks, 256, 0, st>>>(*d, tiles_x, tiles_y, ntiles, tpb);
+      return rdn_check_launch("rdn_conv_wgrad(conv3 glds)");
+    }
+  } else {
+    if constexpr (Geo<BM, CK, false>::OK) {
+      RDN_PROBE("wgrad3_glds_kernel<bf16,%d,%d>", BM, CK);
+      wgrad3_glds_kernel<BM, CK, false><<<blocks, 256, 0, st>>>(*d, tiles_x, tiles_y, ntiles, tpb);
+      return rdn_check_launch("rdn_conv_wgrad(conv3 glds)");
+    }
+  }
+  rdn_set_error("rdn_conv_wgrad(conv3 glds): BM=%d CK=%d does not fit", BM, CK);
+  return RDN_E_SHAPE;
+}
+
+template <int BM>
+int launch_ck(const rdn_wgrad_desc* d, int ck, int blocks, int tiles_x, int tiles_y, int ntiles, int tpb,
+              hipStream_t st) {
+  switch (ck) {
+    case 16: return launch<BM, 16>(d, blocks, tiles_x, tiles_y, ntiles, tpb, st);
+    case 32: return launch<BM, 32>(d, blocks, tiles_x, tiles_y, ntiles, tpb, st);
+    case 48: return launch<BM, 48>(d, blocks, tiles_x, tiles_y, ntiles, tpb, st);
+    case 64: return launch<BM, 64>(d, blocks, tiles_x, tiles_y, ntiles, tpb, st);
+    case 80: return launch<BM, 80>(d, blocks, tiles_x, tiles_y, ntiles, tpb, st);
+    case 96: return launch<BM, 96>(d, blocks, tiles_x, tiles_y, ntiles, tpb, st);
+  }
+  rdn_set_error("rdn_conv_wgrad(conv3 glds): CK=%d", ck);
+  return RDN_E_SHAPE;
 }
 
 }  // namespace
 
 // Tile shape of the LDS-DMA weight-gradient kernel for d, or 0 when it does not
-// apply (fp32, a fused PReLU gate on operand A, channel counts off the grid).
-int rdn_wgrad3_glds_pick(const rdn_wgrad_desc* d, int* bm, int* ck) {
-  static const bool off = [] {
-    const char* e = getenv("RDN_WGLDS");
-    return e && e[0] == '0';
-  }();
-  if (off || d->dtype != RDN_BF16 || d->a_gate || d->mdim < 32 || d->ndim % 32) return 0;
+// apply.  single_chunk: the rows plan reads the whole input pixel row in one
+// channel group (the level-0/1 layers, where the PReLU gate is fused); else the
+// multi-chunk (level-1..3) launches, which never carry the gate.
+int rdn_wgrad3_glds_pick(const rdn_wgrad_desc* d, int single_chunk, int* bm, int* ck) {
+  // RDN_WGLDS: unset = multi-chunk launches only; "0" = never; "l0" = also the
+  // single-chunk level-0/1 ones.  Measured on the train step (r02, same box,
+  // interleaved): the single-chunk kernels are faster alone (32 x 80 gated: 140 ->
+  // 96 us) but one 135-KB-LDS block per CU on the weight-gradient stream keeps the
+  // dgrad chain's blocks off those CUs: 1490 vs 1497 img/s, so they stay opt-in
+  static const char* env = getenv("RDN_WGLDS");
+  const bool off = env && env[0] == '0';
+  const bool no_l0 = !(env && env[0] == 'l');
+  if (off || d->dtype != RDN_BF16) return 0;
+  if (single_chunk) {
+    // 32-row blocks only: the 16-row level-0 layers were equal or slower alone (one
+    // resident block per CU against the rows kernel's two)
+    if (no_l0 || d->mdim <= 16 || d->mdim > 64 || d->ndim > 96 || d->ndim % 16) return 0;
+    *bm = d->mdim <= 16 ? 16 : d->mdim <= 32 ? 32 : 64;
+    *ck = d->ndim;
+    // 64-row blocks only up to 64 channels (the gated 64 x 80 spills, 64 x 96 does not fit)
+    return *bm < 64 || *ck <= 64;
+  }
+  if (d->a_gate || d->mdim < 32 || d->ndim % 32) return 0;
   *bm = d->mdim <= 32 ? 32 : 64;
   *ck = d->ndim % 64 == 0 ? 64 : 32;
   return 1;
@@ -268,10 +431,9 @@ int rdn_wgrad3_glds_pick(const rdn_wgrad_desc* d, int* bm, int* ck) {
 
 int rdn_wgrad3_glds_launch(const rdn_wgrad_desc* d, int bm, int ck, int blocks, int tiles_x, int tiles_y, int ntiles,
                            int tpb, hipStream_t st) {
-  if (bm == 32) return ck == 64 ? launch<32, 64>(d, blocks, tiles_x, tiles_y, ntiles, tpb, st)
-                                : launch<32, 32>(d, blocks, tiles_x, tiles_y, ntiles, tpb, st);
-  if (bm == 64) return ck == 64 ? launch<64, 64>(d, blocks, tiles_x, tiles_y, ntiles, tpb, st)
-                                : launch<64, 32>(d, blocks, tiles_x, tiles_y, ntiles, tpb, st);
-  rdn_set_error("rdn_conv_wgrad(conv3 glds): BM=%d CK=%d", bm, ck);
+  if (bm == 16) return launch_ck<16>(d, ck, blocks, tiles_x, tiles_y, ntiles, tpb, st);
+  if (bm == 32) return launch_ck<32>(d, ck, blocks, tiles_x, tiles_y, ntiles, tpb, st);
+  if (bm == 64) return launch_ck<64>(d, ck, blocks, tiles_x, tiles_y, ntiles, tpb, st);
+  rdn_set_error("rdn_conv_wgrad(conv3 glds): BM=%d", bm);
   return RDN_E_SHAPE;
 }

@@ -570,9 +570,9 @@ Plan plan(const rdn_wgrad_desc* d) {
   p.tiles_x = (d->w + TW - 1) / TW;
   p.tiles_y = (d->h + TH - 1) / TH;
   p.ntiles = d->n * p.tiles_x * p.tiles_y;
-  // multi-chunk launches without the gate: the LDS-DMA pipelined kernel
-  // (wgrad3_glds.hip), one block per CU
-  if (p.rows && p.chunks_rows > 1 && rdn_wgrad3_glds_pick(d, &p.bm, &p.ck)) {
+  // the LDS-DMA pipelined kernel (wgrad3_glds.hip), one block per CU: multi-chunk
+  // launches (no gate) and the single-chunk level-0/1 ones (gate fused)
+  if (p.rows && rdn_wgrad3_glds_pick(d, p.chunks_rows == 1, &p.bm, &p.ck)) {
     p.glds = 1;
     p.mtiles = (d->mdim + p.bm - 1) / p.bm;
     p.chunks = d->ndim / p.ck;
