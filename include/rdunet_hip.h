@@ -188,7 +188,8 @@ int rdn_conv3_packed_k(int32_t cin, int32_t dtype);
 /* output-channel tile the 3x3 kernel uses for `ncols` columns (16..128) */
 int rdn_conv3_pick_bn(int32_t ncols);
 
-/* Many packs in one launch: `items` is a DEVICE array of n rdn_pack_item. */
+/* Many packs in one launch: `items` is a DEVICE array of n rdn_pack_item, each with
+   kp a multiple of 64 and rows_pad * kp < 2^31 (as the engine allocates them). */
 typedef struct rdn_pack_item {
   const float* w; void* out;
   int32_t mode, d0, d1, kh, kw, pad0, pad1, rows_pad, kp, ck;

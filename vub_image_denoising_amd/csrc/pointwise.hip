@@ -273,15 +273,26 @@ __global__ void pack_weights_kernel(int mode, const float* __restrict__ w, int d
   }
 }
 
+// one thread = one 16-byte unit of packed output (kp is a multiple of 64, so a unit
+// never straddles two rows); 32-bit index math (rows_pad * kp < 2^31 per pack).
+// Measured per train step (r02): one element per thread with 64-bit divisions
+// 133 us -> 72 us.  What remains is the gather: consecutive k of a packed row read
+// weights 9 floats apart (OIHW -> [co][tap][ci]); a flattened index space over all
+// packs (per-pack prefix in LDS) was slower (85 us).
 template <typename T>
-__global__ void pack_weights_batched_kernel(const rdn_pack_item* __restrict__ items, int sk) {
+__global__ __launch_bounds__(256) void pack_weights_batched_kernel(const rdn_pack_item* __restrict__ items, int sk) {
+  constexpr int VEC = TypeInfo<T>::VEC;
   const rdn_pack_item it = items[blockIdx.y];
   const int kc = it.ck > 0 ? (9 * it.ck + sk - 1) / sk * sk : 0;
-  const int64_t total = (int64_t)it.rows_pad * it.kp;
+  const int units = it.rows_pad * (it.kp / VEC);
   T* __restrict__ out = (T*)it.out;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int r = (int)(i / it.kp), k = (int)(i - (int64_t)r * it.kp);
-    out[i] = from_f32<T>(pack_value(it.mode, it.w, it.d0, it.d1, it.kh, it.kw, it.pad0, it.pad1, kc, it.ck, r, k));
+  for (int u = blockIdx.x * 256 + threadIdx.x; u < units; u += gridDim.x * 256) {
+    const int e = u * VEC, r = e / it.kp, k0 = e - r * it.kp;
+    float v[VEC];
+#pragma unroll
+    for (int q = 0; q < VEC; ++q)
+      v[q] = pack_value(it.mode, it.w, it.d0, it.d1, it.kh, it.kw, it.pad0, it.pad1, kc, it.ck, r, k0 + q);
+    *(u32x4*)(out + e) = Unit16<T>::pack(v);
   }
 }
 
@@ -536,7 +547,7 @@ extern "C" int rdn_pack_input(int32_t dtype, const float* x, int32_t n, int32_t 
 
 extern "C" int rdn_pack_weights_batched(const rdn_pack_item* items, int32_t n, int32_t dtype, void* stream) {
   if (!items || n <= 0 || n > 65535) { rdn_set_error("rdn_pack_weights_batched: bad arguments"); return RDN_E_ARG; }
-  dim3 grid(64, n);
+  dim3 grid(96, n);   // 96 x 256 units per pass: the largest pack (level-3 conv_3) in ~8 passes
   if (dtype == RDN_BF16) pack_weights_batched_kernel<bf16><<<grid, 256, 0, RDN_STREAM>>>(items, 64);
   else pack_weights_batched_kernel<float><<<grid, 256, 0, RDN_STREAM>>>(items, 32);
   return rdn_check_launch("rdn_pack_weights_batched");
