@@ -403,7 +403,7 @@ int launch_ck(const rdn_wgrad_desc* d, int ck, int blocks, int tiles_x, int tile
 // Tile shape of the LDS-DMA weight-gradient kernel for d, or 0 when it does not
 // apply.  single_chunk: the rows plan reads the whole input pixel row in one
 // channel group (the level-0/1 layers, where the PReLU gate is fused); else the
-// multi-chunk (level-1..3) launches, which never carry the gate.
+// multi-chunk (level-1..3) launches.
 int rdn_wgrad3_glds_pick(const rdn_wgrad_desc* d, int single_chunk, int* bm, int* ck) {
   // RDN_WGLDS: unset = multi-chunk launches only; "0" = never; "l0" = also the
   // single-chunk level-0/1 ones.  Measured on the train step (r02, same box,
@@ -423,7 +423,7 @@ int rdn_wgrad3_glds_pick(const rdn_wgrad_desc* d, int single_chunk, int* bm, int
     // 64-row blocks only up to 64 channels (the gated 64 x 80 spills, 64 x 96 does not fit)
     return *bm < 64 || *ck <= 64;
   }
-  if (d->a_gate || d->mdim < 32 || d->ndim % 32) return 0;
+  if (d->mdim < 32 || d->ndim % 32) return 0;   // (gated here only with RDN_FUSE_MAX_CHUNKS > 1)
   *bm = d->mdim <= 32 ? 32 : 64;
   *ck = d->ndim % 64 == 0 ? 64 : 32;
   return 1;

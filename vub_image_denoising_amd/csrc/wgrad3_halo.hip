@@ -577,7 +577,14 @@ Plan plan(const rdn_wgrad_desc* d) {
     p.mtiles = (d->mdim + p.bm - 1) / p.bm;
     p.chunks = d->ndim / p.ck;
     const int base = p.mtiles * p.chunks;
-    int s = d->splits > 0 ? d->splits : 256 / base;
+    // blocks per launch (RDN_WGLDS_BLOCKS): 192 of the 256 CUs, leaving room beside
+    // the dgrad chain; step A/B (3 interleaved rounds, same box): 128: 1483, 192:
+    // 1506, 256: 1499, 512: 1416 img/s (past 256 the 1-per-CU blocks run in two waves)
+    static const int gtarget = [] {
+      const char* e = getenv("RDN_WGLDS_BLOCKS");
+      return e && atoi(e) > 0 ? atoi(e) : 192;
+    }();
+    int s = d->splits > 0 ? d->splits : gtarget / base;
     const int maxs = (p.ntiles + 1) / 2;                             // >= 2 tiles per block
     if (s > maxs) s = maxs;
     if (s < 1) s = 1;
