@@ -32,7 +32,7 @@ constexpr int ROWB = 160;                  // B-stage row: 128 B + 32 B pad (con
 
 // occupancy request: narrow tiles keep 2 waves/SIMD, wide tiles let the
 // register allocator use up to 512 VGPRs (measured faster: scripts/kbench.py)
-template <typename T, int BN, int WMW, int CK, bool GATE>
+template <typename T, int BN, int WMW, int CK, bool GATE, bool PAIR_OK>
 __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_conv_desc d, int tiles_x, int tiles_y) {
   constexpr int ES = sizeof(T);
   constexpr int VEC = TypeInfo<T>::VEC;
@@ -51,7 +51,16 @@ __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_
   constexpr int B_UNITS = BN * 8;
   constexpr int B_IT = (B_UNITS + NT - 1) / NT;
   constexpr int HALO_BYTES = HW_ * HROW;
-  constexpr int MAIN_BYTES = HALO_BYTES + 2 * BN * ROWB;
+  // PAIR: two consecutive 128-B K stages per LDS stage and barrier (bf16, <= 96
+  // columns: two blocks per CU still fit); a 256-B row padded to 288 B keeps the
+  // ds_read_b128 B fragments conflict-free.  The launcher takes it for grids of at
+  // most two blocks per CU: there halving the barriers wins (level-2 forward -11 %,
+  // level-1 -17 %), on larger grids the single-stage form's third resident block
+  // per CU does (level-2/3 input gradients +10 % when paired)
+  constexpr bool PAIR = PAIR_OK && ES == 2 && BN <= 96 && SPC >= 2;
+  constexpr int RW = PAIR ? 288 : ROWB;              // LDS weight row of one (paired) stage
+  constexpr int SS = PAIR ? (SPC + 1) / 2 : SPC;     // (paired) stages per chunk
+  constexpr int MAIN_BYTES = HALO_BYTES + 2 * BN * RW;
   constexpr int CROW = BN * 4 + 16;                  // epilogue fp32 tile row
   constexpr int EPI_BYTES = BM * CROW;
   constexpr int LDS_BYTES = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
@@ -63,7 +72,7 @@ __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_
 
   __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
   unsigned char* const halo = lds;
-  unsigned char* const bst = lds + HALO_BYTES;      // two weight stages of BN x ROWB
+  unsigned char* const bst = lds + HALO_BYTES;      // two weight stages of BN x RW
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WMW, wn = wave / WMW;
@@ -135,19 +144,30 @@ __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_
       *(u32x4*)(halo + hlds[it]) = v;
     }
   };
-  // ---- weight stages: 8 units (128 B) per output channel; stage (c, j) at c*KC + j*SK
-  u32x4 breg[B_IT];
+  // ---- weight stages: 8 units (128 B) per output channel; stage (c, j) at c*KC + j*SK;
+  // an LDS stage jj holds K stages PAIR ? {2jj, 2jj+1} : {jj}
+  u32x4 breg[PAIR ? 2 : 1][B_IT];
   const int ku = tid & 7;
   const T* const wb = (const T*)d.wp + (int64_t)(n0 + (tid >> 3)) * d.kp + ku * VEC;
-  auto load_b = [&](int c, int j) {
+  auto load_b = [&](int c, int jj) {
 #pragma unroll
-    for (int it = 0; it < B_IT; ++it)
-      if (tid + it * NT < B_UNITS) breg[it] = *(const u32x4*)(wb + (int64_t)it * (NT / 8) * d.kp + c * KC + j * SK);
+    for (int h = 0; h < (PAIR ? 2 : 1); ++h) {
+      const int j = PAIR ? 2 * jj + h : jj;
+      if (j >= SPC) break;
+#pragma unroll
+      for (int it = 0; it < B_IT; ++it)
+        if (tid + it * NT < B_UNITS) breg[h][it] = *(const u32x4*)(wb + (int64_t)it * (NT / 8) * d.kp + c * KC + j * SK);
+    }
   };
-  auto store_b = [&](int buf) {
+  auto store_b = [&](int buf, int jj) {
 #pragma unroll
-    for (int it = 0; it < B_IT; ++it)
-      if (tid + it * NT < B_UNITS) *(u32x4*)(bst + buf * (BN * ROWB) + ((tid >> 3) + it * (NT / 8)) * ROWB + ku * 16) = breg[it];
+    for (int h = 0; h < (PAIR ? 2 : 1); ++h) {
+      if ((PAIR ? 2 * jj + h : jj) >= SPC) break;
+#pragma unroll
+      for (int it = 0; it < B_IT; ++it)
+        if (tid + it * NT < B_UNITS)
+          *(u32x4*)(bst + buf * (BN * RW) + ((tid >> 3) + it * (NT / 8)) * RW + h * 128 + ku * 16) = breg[h][it];
+    }
   };
 
   // ---- fragment addresses: per-lane base + immediates
@@ -164,7 +184,7 @@ __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_
     }
   }
   const unsigned char* const pa = halo + (KALIGN ? a_lane + g * 16 : 0);
-  const int b_lane = (wn * WTN + r) * ROWB + g * 16;
+  const int b_lane = (wn * WTN + r) * RW + g * 16;
 
   f32x4 acc[MT][NTL];
 #pragma unroll
@@ -189,7 +209,7 @@ __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_
 #pragma unroll
       for (int i = 0; i < MT; ++i) af[i] = *(const u32x4*)(pa + ao + i * (TW + 2) * HROW);
 #pragma unroll
-      for (int jn = 0; jn < NTL; ++jn) bfr[jn] = *(const u32x4*)(pbs + jn * 16 * ROWB + ks * 64);
+      for (int jn = 0; jn < NTL; ++jn) bfr[jn] = *(const u32x4*)(pbs + jn * 16 * RW + ks * 64);
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -211,18 +231,23 @@ __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_
   load_halo(0);
   load_b(0, 0);
   store_halo();
-  store_b(0);
+  store_b(0, 0);
   __syncthreads();
   int buf = 0;
   for (int c = 0; c < nch; ++c) {
     const bool more = c + 1 < nch;
-    if (more) load_halo(c + 1);   // in flight during this chunk's SPC stages
+    if (more) load_halo(c + 1);   // in flight during this chunk's stages
 #pragma unroll
-    for (int j = 0; j < SPC; ++j) {
-      const bool nxt = j + 1 < SPC || more;
-      if (nxt) load_b(j + 1 < SPC ? c : c + 1, j + 1 < SPC ? j + 1 : 0);
-      compute(j, bst + buf * (BN * ROWB) + b_lane);
-      if (nxt) store_b(buf ^ 1);
+    for (int jj = 0; jj < SS; ++jj) {
+      const bool nxt = jj + 1 < SS || more;
+      if (nxt) load_b(jj + 1 < SS ? c : c + 1, jj + 1 < SS ? jj + 1 : 0);
+      if constexpr (PAIR) {
+        compute(2 * jj, bst + buf * (BN * RW) + b_lane);
+        if (2 * jj + 1 < SPC) compute(2 * jj + 1, bst + buf * (BN * RW) + b_lane + 128);
+      } else {
+        compute(jj, bst + buf * (BN * RW) + b_lane);
+      }
+      if (nxt) store_b(buf ^ 1, jj + 1 < SS ? jj + 1 : 0);
       __syncthreads();
       buf ^= 1;
     }
@@ -313,17 +338,32 @@ __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_
 template <typename T, int BN, int WMW, int CK>
 int launch_h(const rdn_conv_desc* d, hipStream_t st) {
   const int tiles_x = (d->w + TW - 1) / TW, tiles_y = (d->h + TH - 1) / TH;
-  dim3 grid((unsigned)(d->n * tiles_x * tiles_y * ((d->ncols + BN - 1) / BN)));
-  RDN_PROBE("conv3_halo_kernel<%s,%d,%d,%d%s>", rdn_tname<T>(), BN, WMW, CK, d->gate ? ",gate" : "");
+  const int64_t blocks = (int64_t)d->n * tiles_x * tiles_y * ((d->ncols + BN - 1) / BN);
+  dim3 grid((unsigned)blocks);
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
+  }
+  static const bool no_pair = [] {
+    const char* e = getenv("RDN_HALO_PAIR");
+    return e && e[0] == '0';
+  }();
+  const bool pair = !no_pair && blocks <= 2 * (int64_t)cus;
+  RDN_PROBE("conv3_halo_kernel<%s,%d,%d,%d%s%s>", rdn_tname<T>(), BN, WMW, CK, d->gate ? ",gate" : "",
+            pair && sizeof(T) == 2 && BN <= 96 ? ",pair" : "");
   if (d->gate) {
-    if constexpr (NT % (CK / TypeInfo<T>::VEC) == 0)
-      conv3_halo_kernel<T, BN, WMW, CK, true><<<grid, NT, 0, st>>>(*d, tiles_x, tiles_y);
-    else {
+    if constexpr (NT % (CK / TypeInfo<T>::VEC) == 0) {
+      if (pair) conv3_halo_kernel<T, BN, WMW, CK, true, true><<<grid, NT, 0, st>>>(*d, tiles_x, tiles_y);
+      else conv3_halo_kernel<T, BN, WMW, CK, true, false><<<grid, NT, 0, st>>>(*d, tiles_x, tiles_y);
+    } else {
       rdn_set_error("rdn_conv_fwd(conv3): gated input needs a power-of-two channel chunk");
       return RDN_E_SHAPE;
     }
   } else {
-    conv3_halo_kernel<T, BN, WMW, CK, false><<<grid, NT, 0, st>>>(*d, tiles_x, tiles_y);
+    if (pair) conv3_halo_kernel<T, BN, WMW, CK, false, true><<<grid, NT, 0, st>>>(*d, tiles_x, tiles_y);
+    else conv3_halo_kernel<T, BN, WMW, CK, false, false><<<grid, NT, 0, st>>>(*d, tiles_x, tiles_y);
   }
   return rdn_check_launch("rdn_conv_fwd(conv3)");
 }
