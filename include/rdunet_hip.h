@@ -24,6 +24,7 @@
  *                     (aten convolution_backward, grad_input).
  *   rdn_conv_wgrad /  aten convolution_backward grad_weight for the same convs.
  *   rdn_wgrad_reduce
+ *   rdn_conv_dgrad_wgrad  both of the above for one gated level-0 conv in one pass.
  *   rdn_prelu_bwd     aten _prelu_kernel_backward (dx, dalpha) + conv grad_bias.
  *   rdn_interp        x = a*noisy + (1-a)*clean, diffusion_RDUnet.py:90-100, :33-36.
  *   rdn_pack_input    torch.cat((inputs, t.expand(...)), 1), Unet_model.py:135-136.
@@ -141,6 +142,21 @@ int64_t rdn_wgrad_workspace_size(const rdn_wgrad_desc* d);
 int rdn_wgrad_reduce(const float* ws, int32_t splits, int32_t mdim, int32_t ndim, int32_t ndim_real,
                      int32_t taps, float* grad, int32_t accumulate,
                      const float* part, int32_t part_splits, float* dalpha, float* dbias, void* stream);
+
+/* Fused input gradient + weight gradient of one gated 3x3 conv (the narrow level-0
+   layers: dgrad->cin = 16|32 dY channels, dgrad->ncols = wgrad->ndim = 32..80 input
+   channels, full 8x16 tiles, bf16): ONE pass over the gated dY (dgrad->gate must be
+   set and equal wgrad->a_gate; wgrad->a must be dgrad->x) computes
+   rdn_conv_fwd(dgrad) and rdn_conv_wgrad(wgrad) together, i.e. aten
+   convolution_backward's grad_input and grad_weight of Unet_model.py:72-89 with
+   _prelu_kernel_backward fused.  wgrad->splits must equal
+   rdn_conv_dgrad_wgrad_splits(); sum with rdn_wgrad_reduce as usual.
+   Returns 0 (launched), 1 (pair not served: launch the two separately) or < 0. */
+int rdn_conv_dgrad_wgrad(const rdn_conv_desc* dgrad, const rdn_wgrad_desc* wgrad, void* stream);
+/* split count (weight-gradient slabs) the fused kernel writes for the pair; 0 = not served */
+int rdn_conv_dgrad_wgrad_splits(const rdn_conv_desc* dgrad, const rdn_wgrad_desc* wgrad);
+/* name of the fused kernel instantiation (1 = not served) */
+int rdn_conv_dgrad_wgrad_kernel_name(const rdn_conv_desc* dgrad, const rdn_wgrad_desc* wgrad, char* buf, int32_t len);
 
 /* PReLU backward (+ conv bias gradient) over a pixel grid of `pixels` pixels:
    dyp[p, c] = dy[p, c] * (pre[p, c] > 0 ? 1 : alpha[c])   (c < C; 0 for C <= c < cpad)

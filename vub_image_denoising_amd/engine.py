@@ -192,6 +192,9 @@ SERIAL_BWD = False
 # cb = F_l/2 (one plane per dense-block growth slice), so a conv reading or writing a
 # channel slice touches only its planes (include/rdunet_hip.h, *_pl fields)
 PLANAR = os.environ.get("RDN_PLANAR", "1") != "0"
+# gated level-0 convs: input + weight gradient in one fused kernel on the compute
+# stream (rdn_conv_dgrad_wgrad) instead of dgrad there and wgrad on the side stream
+FUSE_DW = os.environ.get("RDN_DW", "1") != "0"
 # extra elements between two planes (keeps plane starts off power-of-two strides)
 PLANE_PAD = int(os.environ.get("RDN_PLANE_PAD", "0"))
 
@@ -641,6 +644,7 @@ class UNetEngine:
     def _build_bwd(self):
         lib = H.lib()
         ws_need = 0
+        dw_need = 0
         part_need = 0
         for b, L in enumerate(reversed(self.layers)):   # backward order -> ring slot
             L.extra["slot"] = b % self.slots
@@ -727,7 +731,15 @@ class UNetEngine:
             wg.splits = 0
             splits = lib.rdn_wgrad_splits(C.byref(wg))
             wg.splits = splits
-            ws_need = max(ws_need, lib.rdn_wgrad_workspace_size(C.byref(wg)))
+            dw = 0
+            if fused and FUSE_DW and L.src.buf not in self.pure_inputs:
+                dw = lib.rdn_conv_dgrad_wgrad_splits(C.byref(d), C.byref(wg))
+            L.extra["dw"] = dw > 0
+            if dw > 0:   # the fused kernel's slabs: one per block of its persistent grid
+                splits = wg.splits = dw
+                dw_need = max(dw_need, dw * wg.mdim * 9 * wg.ndim * 4)
+            else:
+                ws_need = max(ws_need, lib.rdn_wgrad_workspace_size(C.byref(wg)))
             if fused:
                 part_need = max(part_need, splits * 2 * wg.mdim * 4)
             L.wgrad_desc = wg
@@ -737,11 +749,16 @@ class UNetEngine:
             L.extra["goff"] = [4 * self.fp.offsets[i] for i in pidx]   # byte offsets in a flat gradient buffer
             L.extra["olvl"] = olvl
         self.ws = torch.zeros(max(ws_need // 4, 4), dtype=torch.float32, device=self.device)
+        # fused layers write their slabs from the compute stream while the side stream
+        # may still reduce an earlier layer's: one workspace per ring slot, released by
+        # the same ev_done wait that releases the slot's partials
+        self.ws_dw = (torch.zeros(self.slots, (dw_need // 4 + 3) // 4 * 4, dtype=torch.float32, device=self.device)
+                      if dw_need else None)
         pws = max(part_need, self.pws_bytes, 16) // 4
         self.pws = torch.zeros(self.slots, (pws + 3) // 4 * 4, dtype=torch.float32, device=self.device)
         for L in self.layers:
             L.extra["pws"] = self.pws[L.extra["slot"]].data_ptr()
-            L.wgrad_desc.ws = self.ws.data_ptr()
+            L.wgrad_desc.ws = self.ws_dw[L.extra["slot"]].data_ptr() if L.extra["dw"] else self.ws.data_ptr()
             if L.extra["fused"]:
                 L.wgrad_desc.part = L.extra["pws"]
         if self.side is not None:   # per layer: dYpre ready (compute stream) / slot free (side stream)
@@ -776,6 +793,14 @@ class UNetEngine:
         H.check(H.lib().rdn_wgrad_kernel_name(C.byref(d), buf, 128), "rdn_wgrad_kernel_name")
         return buf.value.decode()
 
+    def _dw_key(self, d, wg):
+        dc = self._probe_copy(d, H.ConvDesc, ("gate", "gate_alpha"))
+        wc = self._probe_copy(wg, H.WgradDesc, ("a_gate", "a_gate_alpha", "part"))
+        buf = C.create_string_buffer(128)
+        H.check(H.lib().rdn_conv_dgrad_wgrad_kernel_name(C.byref(dc), C.byref(wc), buf, 128),
+                "rdn_conv_dgrad_wgrad_kernel_name")
+        return buf.value.decode()
+
     def _build_info(self):
         """Per launch: kernel instantiation key + algorithmic FLOPs and bytes
         (each operand read once, each output written once)."""
@@ -800,6 +825,9 @@ class UNetEngine:
                 info["dgrad"] = ("dgrad", L.name, self._kernel_key(L.dgrad_desc), 2 * macs, dg_bytes)
                 info["wgrad"] = ("wgrad", L.name, self._wgrad_key(L.wgrad_desc), 2 * macs,
                                  es * (Pout * L.cout + gate + Pin * L.cin))
+                if L.extra.get("dw"):   # one pass: dY + gate + X read once, dX written
+                    info["dw"] = ("dwgrad", L.name, self._dw_key(L.dgrad_desc, L.wgrad_desc), 4 * macs,
+                                  dg_bytes + es * Pin * L.cin)
             L.extra["info"] = info
 
     # ------------------------------------------------------------------
@@ -909,27 +937,44 @@ class UNetEngine:
                                            self.named[L.act + ".weight"].data_ptr(), dyp, None, None, pws, st)
             if rc:
                 H.check(rc, f"prelu_bwd[{L.name}]")
-            if side is not None:
-                L.extra["ev_ready"].record(main)
-            if L.src.buf not in self.pure_inputs or need_buf[L.src.buf]:
-                tok = tr.start(info["dgrad"]) if tr is not None else None
-                rc = lib.rdn_conv_fwd(C.byref(L.dgrad_desc), st)
+            dw = L.extra["dw"]
+            if dw:
+                # fused input + weight gradient on the compute stream; its slabs and
+                # partials go to this ring slot's buffers, free once the side stream
+                # reduced the layer that used the slot before
+                if side is not None and b >= self.slots:
+                    main.wait_event(rev[b - self.slots].extra["ev_done"])
+                tok = tr.start(info["dw"]) if tr is not None else None
+                rc = lib.rdn_conv_dgrad_wgrad(C.byref(L.dgrad_desc), C.byref(L.wgrad_desc), st)
                 if tok is not None:
                     tr.stop(tok)
                 if rc:
-                    H.check(rc, f"dgrad[{L.name}]")
+                    H.check(rc, f"dgrad_wgrad[{L.name}]")
+                if side is not None:
+                    L.extra["ev_ready"].record(main)
+            else:
+                if side is not None:
+                    L.extra["ev_ready"].record(main)
+                if L.src.buf not in self.pure_inputs or need_buf[L.src.buf]:
+                    tok = tr.start(info["dgrad"]) if tr is not None else None
+                    rc = lib.rdn_conv_fwd(C.byref(L.dgrad_desc), st)
+                    if tok is not None:
+                        tr.stop(tok)
+                    if rc:
+                        H.check(rc, f"dgrad[{L.name}]")
             if side is not None:
                 side.wait_event(L.extra["ev_ready"])
-            tok = tr.start(info["wgrad"], side) if tr is not None else None
-            rc = lib.rdn_conv_wgrad(C.byref(L.wgrad_desc), sst)
-            if tok is not None:
-                tr.stop(tok)
-            if rc:
-                H.check(rc, f"wgrad[{L.name}]")
+            if not dw:
+                tok = tr.start(info["wgrad"], side) if tr is not None else None
+                rc = lib.rdn_conv_wgrad(C.byref(L.wgrad_desc), sst)
+                if tok is not None:
+                    tr.stop(tok)
+                if rc:
+                    H.check(rc, f"wgrad[{L.name}]")
             splits, mdim, ndim, ndim_real, taps = L.extra["wgrad"]
             part_splits = 0 if fused else lib.rdn_prelu_bwd_blocks(self.code, P, L.cout_pad)
             ow, ob, oa = L.extra["goff"]
-            rc = lib.rdn_wgrad_reduce(self.ws.data_ptr(), splits, mdim, ndim, ndim_real, taps, gbase + ow, 1, pws,
+            rc = lib.rdn_wgrad_reduce(L.wgrad_desc.ws, splits, mdim, ndim, ndim_real, taps, gbase + ow, 1, pws,
                                       part_splits, gbase + oa, gbase + ob, sst)
             if rc:
                 H.check(rc, f"wgrad_reduce[{L.name}]")
