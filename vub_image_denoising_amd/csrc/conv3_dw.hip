@@ -24,12 +24,22 @@
 //          ds_read_b64_tr_b16 (same k order as wgrad3_rows: lane group g takes
 //          pixels 4g..4g+3 then 16+4g..16+4g+3 of a 32-pixel k-step).
 //
-// Persistent grid, one 8-wave block per CU, XCD-local tile ranges (as conv3_ws);
-// the weight-gradient accumulators stay in registers over the block's tiles and
-// the block writes ONE split-K slab at the end (split = block), summed with the
-// dalpha/dbias partials by rdn_wgrad_reduce in fixed order (deterministic).  The
-// next tile's halos (and the epilogue's residual / accumulate operands) are in
-// flight in registers while the current tile computes.
+// Persistent grid, one 8-wave block per CU, XCD-local tile ranges (as conv3_ws).
+// The waves split by role, so each role's registers fit two tiles of loads in
+// flight (the layers are HBM-latency bound: with one tile in flight the v1 of this
+// kernel spent 120 of its 200 us in the load -> barrier chain, measured with the
+// MFMAs and stores switched off):
+//
+//   waves 0-3 (D): gated dY halo loads (+ the PReLU-backward gate and dalpha/dbias
+//     partials on the way to LDS), dgrad MFMAs (32 pixels x BN per wave), the dX
+//     epilogue (residual / accumulate operand prefetched one tile ahead);
+//   waves 4-7 (W): X halo loads, wgrad MFMAs (n-tiles w, w+4, ...), accumulators in
+//     registers over the block's tiles; ONE split-K slab per block at the end
+//     (split = block), summed with the partials by rdn_wgrad_reduce in fixed order.
+//
+// Every global load in the tile loop is unconditional (out-of-image units read a
+// zero line), so the compiler's vmcnt waits count exactly and the wait for tile
+// t+1 does not drain tile t+2's loads.
 #include "conv3_tile.h"
 
 #include <stdlib.h>
@@ -56,32 +66,53 @@ struct DwCfg {
   static constexpr int X_BYTES = (HW_ * XROW + 15) / 16 * 16;
   static constexpr int CROWF = BN + 4;                  // epilogue fp32 row (floats)
   static constexpr int CT_BYTES = BM * CROWF * 4;
-  static constexpr int RED_BYTES = 2 * NT * 8 * 4;      // dalpha/dbias partial reduction (aliases)
+  static constexpr int RED_BYTES = 2 * 256 * 8 * 4;     // dalpha/dbias partial reduction (aliases)
   static constexpr int AL_BYTES = (CK * 4 + 15) / 16 * 16;   // gate slopes
   static constexpr int LDS = W_BYTES + D_BYTES + X_BYTES + CT_BYTES + AL_BYTES;
   static constexpr bool FITS = LDS <= LDS_MAX && D_BYTES + X_BYTES + CT_BYTES >= RED_BYTES;
 };
 
+// 16-byte load through a buffer descriptor on a wave-uniform base: a byte offset
+// past the descriptor's range (OOB) returns zeros -- halo padding without branches,
+// so the compiler's vmcnt waits stay exact (a predicated flat load became a branch
+// with a vmcnt(0) inside)
+constexpr int OOB = 0x7ffffff0;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* base) {
+  const uint64_t a = (uint64_t)(uintptr_t)base;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a), hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | lo), 0, OOB, 0x00020000);
+}
+__device__ __forceinline__ u32x4 ld16(__amdgpu_buffer_rsrc_t rs, bool ok, int off_bytes) {
+  int o = ok ? off_bytes : OOB;
+  asm volatile("" : "+v"(o));   // opaque: keeps ONE load (hipcc otherwise splits it into two predicated ones)
+  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0));
+}
+
 template <int BN, int CK>
 __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wgrad_desc wg, int tiles_x, int tiles_y,
-                                                         int ntiles, int dbg) {
+                                                         int ntiles) {
   using Cfg = DwCfg<BN, CK>;
   constexpr int VEC = 8;
   constexpr int KC = Cfg::KC, NSTEP = Cfg::NSTEP, WROW = Cfg::WROW, DROW = Cfg::DROW, XROW = Cfg::XROW;
   constexpr int CROWF = Cfg::CROWF;
+  constexpr int NR = 256;                               // threads per role
+  constexpr int MT = 2;                                 // dgrad: 2 x 16 pixels per D wave
   constexpr int NTL = BN / 16;                          // dgrad n-tiles
   constexpr int DU = CK / VEC, XU = BN / VEC;           // 16-B units per halo pixel
   constexpr int D_UNITS = HW_ * DU, X_UNITS = HW_ * XU;
-  constexpr int D_IT = (D_UNITS + NT - 1) / NT, X_IT = (X_UNITS + NT - 1) / NT;
+  constexpr int D_IT = (D_UNITS + NR - 1) / NR, X_IT = (X_UNITS + NR - 1) / NR;
   constexpr int MTW = CK / 16;                          // wgrad m-tiles
   constexpr int NT_ALL = 9 * BN / 16;                   // wgrad n-tiles
-  constexpr int NTW = (NT_ALL + 7) / 8;                 // per wave (n-tile = wave + 8 j)
-  constexpr int UPR = BN / VEC, EU = BM * UPR, E_IT = (EU + NT - 1) / NT;
+  constexpr int NTW = (NT_ALL + 3) / 4;                 // per W wave (n-tile = wave + 4 j)
+  constexpr int UPR = BN / VEC, EU = BM * UPR, E_IT = (EU + NR - 1) / NR;
   constexpr bool KALIGN = CK % 32 == 0;                 // a dgrad k-step never straddles a tap
   constexpr int RS = (TW + 2);                          // halo pixels per halo row
-  static_assert(NT % DU == 0, "fixed dY channel group per thread");
+  static_assert(NR % DU == 0, "fixed dY channel group per thread");
   static_assert(BN % 16 == 0 && CK % 16 == 0, "16-wide MFMA tiles");
   static_assert(Cfg::FITS, "LDS");
+  // W waves keep two X halos in flight where the registers allow it (accumulators
+  // MTW x NTW x 4 + two X_IT sets within the 256-VGPR budget of 2 waves / SIMD)
+  constexpr bool DW2 = MTW * NTW * 4 + 2 * X_IT * 4 <= 112;
 
   __shared__ __attribute__((aligned(16))) unsigned char lds[Cfg::LDS];
   unsigned char* const wl = lds;
@@ -91,6 +122,8 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
   float* const alds = (float*)(xh + Cfg::X_BYTES + Cfg::CT_BYTES);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bool dwave = wave < 4;                          // role (wave-uniform)
+  const int rt = tid & (NR - 1), rw = wave & 3;         // thread / wave within the role
   const int r = lane & 15, g = lane >> 4;
   const int H = d.h, W = d.w;
   const int flags = d.flags;
@@ -98,8 +131,10 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
   // this block's tiles: XCD share, strided by the XCD's block count (conv3_ws)
   const int per = gridDim.x >> 3;
   const int xcd = blockIdx.x & 7;
+  const int t_lo = (int)((int64_t)ntiles * xcd / 8);
   const int t_hi = (int)((int64_t)ntiles * (xcd + 1) / 8);
-  int t = (int)((int64_t)ntiles * xcd / 8) + (blockIdx.x >> 3);
+  int t = t_lo + (blockIdx.x >> 3);
+  const int t_last = t_hi - 1;                          // loads of a tile past the range re-read this one
 
   const bf16* __restrict__ DY = (const bf16*)d.x;
   const bf16* __restrict__ PR = (const bf16*)d.gate;
@@ -116,51 +151,6 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     for (int c = tid; c < CK; c += NT) alds[c] = d.gate_alpha[c];
   }
 
-  // ---- loader geometry (tile-invariant): dY + gate pixel-major with a fixed channel
-  // group per thread; X plane-major when channel-blocked (a load instruction walks
-  // consecutive pixels of one plane)
-  const int dcu = tid % DU;
-  int drel[D_IT], grel[D_IT], dhp[D_IT];
-  unsigned dint = 0;   // bit it: unit `it` is a tile-interior pixel (counted in the partials)
-#pragma unroll
-  for (int it = 0; it < D_IT; ++it) {
-    const int u = tid + it * NT;
-    const int hp = u < D_UNITS ? u / DU : HW_ - 1;
-    const int hy = hp / RS, hx = hp - hy * RS;
-    dhp[it] = hp;
-    drel[it] = (hy * W + hx) * (int)d.x_ps + rdn_coff32(d.x_c0 + dcu * VEC, (int)d.x_ps, (int)d.x_pl);
-    grel[it] = (hy * W + hx) * (int)d.gate_ps + rdn_coff32(dcu * VEC, (int)d.gate_ps, (int)d.gate_pl);
-    if (u < D_UNITS && hy >= 1 && hy <= TH && hx >= 1 && hx <= TW) dint |= 1u << it;
-  }
-  const int xupp = (wg.b_pl && wg.b_c0 % wg.b_ps == 0 && XU % (wg.b_ps / VEC) == 0) ? (int)(wg.b_ps / VEC) : XU;
-  int xrel[X_IT], xlds[X_IT];
-#pragma unroll
-  for (int it = 0; it < X_IT; ++it) {
-    const int u = tid + it * NT;
-    const int pln = u / (HW_ * xupp), rem = u - pln * (HW_ * xupp);
-    const int hp = u < X_UNITS ? rem / xupp : HW_ - 1, cu = u < X_UNITS ? pln * xupp + rem % xupp : 0;
-    const int hy = hp / RS, hx = hp - hy * RS;
-    xrel[it] = (hy * W + hx) * (int)wg.b_ps + rdn_coff32(wg.b_c0 + cu * VEC, (int)wg.b_ps, (int)wg.b_pl);
-    xlds[it] = hp * XROW + cu * 16;
-  }
-  float sa[VEC], sb[VEC];
-#pragma unroll
-  for (int q = 0; q < VEC; ++q) {
-    sa[q] = 0.f;
-    sb[q] = 0.f;
-  }
-
-  // ---- epilogue units (dX): pixel offset in the tile + channel
-  int erel[E_IT], ecol[E_IT];
-#pragma unroll
-  for (int it = 0; it < E_IT; ++it) {
-    const int u = tid + it * NT;
-    const int px = u / UPR;
-    erel[it] = (px / TW) * W + px % TW;
-    ecol[it] = (u - px * UPR) * VEC;
-  }
-  const bool has_res = flags & RDN_EPI_RESID, has_acc = flags & RDN_EPI_ACCUM;
-
   auto origin = [&](int tt, int& oy, int& ox, int& on) {
     const int tx = tt % tiles_x;
     tt /= tiles_x;
@@ -168,269 +158,352 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     ox = tx * TW;
     on = tt / tiles_y;
   };
-  auto load_halos = [&](int oy, int ox, int on, u32x4 (&dr)[D_IT], u32x4 (&gr)[D_IT], u32x4 (&xr)[X_IT]) {
-    const int64_t hpix0 = ((int64_t)on * H + (oy - 1)) * W + (ox - 1);
-    const bf16* const db = DY + hpix0 * d.x_ps;
-    const bf16* const gb = PR + hpix0 * d.gate_ps;
-    const bf16* const xb = XS + hpix0 * wg.b_ps;
-    const bool interior = oy >= 1 && oy + TH + 1 <= H && ox >= 1 && ox + TW + 1 <= W;
-#pragma unroll
-    for (int it = 0; it < D_IT; ++it) {
-      bool ok = (it + 1 < D_IT) || tid + it * NT < D_UNITS;
-      if (!interior) {
-        const int hy = dhp[it] / RS, hx = dhp[it] - (dhp[it] / RS) * RS;
-        ok = ok && (unsigned)(oy - 1 + hy) < (unsigned)H && (unsigned)(ox - 1 + hx) < (unsigned)W;
-      }
-      u32x4 v = {0u, 0u, 0u, 0u}, gv = {0u, 0u, 0u, 0u};
-      if (ok) {
-        v = *(const u32x4*)(db + drel[it]);
-        gv = *(const u32x4*)(gb + grel[it]);
-      }
-      dr[it] = v;
-      gr[it] = gv;
-    }
-#pragma unroll
-    for (int it = 0; it < X_IT; ++it) {
-      bool ok = (it + 1 < X_IT) || tid + it * NT < X_UNITS;
-      if (!interior) {
-        const int hp = xlds[it] / XROW;
-        const int hy = hp / RS, hx = hp - hy * RS;
-        ok = ok && (unsigned)(oy - 1 + hy) < (unsigned)H && (unsigned)(ox - 1 + hx) < (unsigned)W;
-      }
-      u32x4 v = {0u, 0u, 0u, 0u};
-      if (ok) v = *(const u32x4*)(xb + xrel[it]);
-      xr[it] = v;
-    }
+  // halo unit inside the image (pure VALU: a uniform short cut here made the compiler
+  // unswitch the loads into branches with vmcnt(0) waits)
+  auto in_img = [&](int hp, int oy, int ox) {
+    const int hy = hp / RS, hx = hp - (hp / RS) * RS;
+    return (hp < HW_) & ((unsigned)(oy - 1 + hy) < (unsigned)H) & ((unsigned)(ox - 1 + hx) < (unsigned)W);
   };
-  // registers -> LDS; the PReLU-backward gate and the dalpha/dbias partials of the
-  // tile-interior pixels (each image pixel is interior to exactly one tile)
-  auto store_halos = [&](const u32x4 (&dr)[D_IT], const u32x4 (&gr)[D_IT], const u32x4 (&xr)[X_IT]) {
+
+  // The two roles run separate loops (their loop-carried registers do not overlap)
+  // with the same barriers per tile.  At the top of a step LDS holds tile t and the
+  // register set `cur` holds tile t + per in flight; the step issues t + 2 per into
+  // `nxt` (past the range it re-reads the last tile: every load is unconditional).
+  if (dwave) {
+    // ================= D waves: gated dY halo, dgrad, dX epilogue
+    const int dcu = rt % DU;
+    int lrel[D_IT], grel[D_IT], llds[D_IT], uhp[D_IT];
+    unsigned dint = 0;   // bit it: unit `it` is a tile-interior pixel (counted in the partials)
 #pragma unroll
     for (int it = 0; it < D_IT; ++it) {
-      if (it + 1 == D_IT && tid + it * NT >= D_UNITS) continue;
-      float dy[VEC], pr[VEC];
-      Unit16<bf16>::unpack(dr[it], dy);
-      Unit16<bf16>::unpack(gr[it], pr);
-      const bool in = (dint >> it) & 1u;
+      const int u = rt + it * NR;
+      const int hp = u < D_UNITS ? u / DU : HW_;
+      const int hq = hp < HW_ ? hp : 0;
+      const int hy = hq / RS, hx = hq - hy * RS;
+      uhp[it] = hp;
+      lrel[it] = (hy * W + hx) * (int)d.x_ps + rdn_coff32(d.x_c0 + dcu * VEC, (int)d.x_ps, (int)d.x_pl);
+      grel[it] = (hy * W + hx) * (int)d.gate_ps + rdn_coff32(dcu * VEC, (int)d.gate_ps, (int)d.gate_pl);
+      llds[it] = hq * DROW + dcu * 16;
+      if (hp < HW_ && hy >= 1 && hy <= TH && hx >= 1 && hx <= TW) dint |= 1u << it;
+    }
+    float sa[VEC], sb[VEC];
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) {
+      sa[q] = 0.f;
+      sb[q] = 0.f;
+    }
+    // epilogue units (dX): pixel offset in the tile + channel; the operand is the
+    // residual (channels < res_climit) or the accumulated output
+    int erel[E_IT], ecol[E_IT], eoff[E_IT];
+    bool eok[E_IT];
+    const bool has_res = flags & RDN_EPI_RESID, has_acc = flags & RDN_EPI_ACCUM;
+    const bf16* const ebase = has_res ? (const bf16*)d.res : (const bf16*)d.out;
+    const int eps = has_res ? (int)d.res_ps : (int)d.out_ps;
+#pragma unroll
+    for (int it = 0; it < E_IT; ++it) {
+      const int u = rt + it * NR;
+      const int px = u / UPR;
+      erel[it] = (px / TW) * W + px % TW;
+      const int c = ecol[it] = (u - px * UPR) * VEC;
+      eok[it] = (u < EU) && (has_res ? c < d.res_climit : has_acc);
+      eoff[it] = erel[it] * eps + (has_res ? rdn_coff32(d.res_c0 + c, (int)d.res_ps, (int)d.res_pl)
+                                           : rdn_coff32(d.out_c0 + c, (int)d.out_ps, (int)d.out_pl));
+    }
+    auto load = [&](int tt, u32x4 (&lr)[D_IT], u32x4 (&gr)[D_IT]) {
+      int oy, ox, on;
+      origin(tt, oy, ox, on);
+      const int64_t hpix0 = ((int64_t)on * H + (oy - 1)) * W + (ox - 1);
+      const __amdgpu_buffer_rsrc_t rd = rsrc_of(DY + hpix0 * d.x_ps), rg = rsrc_of(PR + hpix0 * d.gate_ps);
+#pragma unroll
+      for (int it = 0; it < D_IT; ++it) {
+        const bool ok = in_img(uhp[it], oy, ox);
+        lr[it] = ld16(rd, ok, lrel[it] * 2);
+        gr[it] = ld16(rg, ok, grel[it] * 2);
+      }
+    };
+    // registers -> LDS with the PReLU-backward gate and the dalpha/dbias partials of
+    // the tile-interior pixels (each image pixel is interior to exactly one tile)
+    auto store = [&](const u32x4 (&lr)[D_IT], const u32x4 (&gr)[D_IT], bool live) {
       const f32x4 a0 = *(const f32x4*)(alds + dcu * VEC), a1 = *(const f32x4*)(alds + dcu * VEC + 4);
 #pragma unroll
-      for (int q = 0; q < VEC; ++q) {
-        const bool pos = pr[q] > 0.f;
-        if (in && !pos) sa[q] += pr[q] * dy[q];
-        dy[q] = pos ? dy[q] : (q < 4 ? a0[q] : a1[q - 4]) * dy[q];
-        if (in) sb[q] += dy[q];
+      for (int it = 0; it < D_IT; ++it) {
+        if (uhp[it] >= HW_) continue;
+        float dy[VEC], pr[VEC];
+        Unit16<bf16>::unpack(lr[it], dy);
+        Unit16<bf16>::unpack(gr[it], pr);
+        const bool in = live && ((dint >> it) & 1u);   // a re-read past the range counts nothing
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) {
+          const bool pos = pr[q] > 0.f;
+          if (in && !pos) sa[q] += pr[q] * dy[q];
+          dy[q] = pos ? dy[q] : (q < 4 ? a0[q] : a1[q - 4]) * dy[q];
+          if (in) sb[q] += dy[q];
+        }
+        *(u32x4*)(dyh + llds[it]) = Unit16<bf16>::pack(dy);
       }
-      *(u32x4*)(dyh + dhp[it] * DROW + dcu * 16) = Unit16<bf16>::pack(dy);
+    };
+    auto load_epi = [&](int tt, u32x4 (&eo)[E_IT]) {
+      int oy, ox, on;
+      origin(tt, oy, ox, on);
+      const __amdgpu_buffer_rsrc_t rb = rsrc_of(ebase + (((int64_t)on * H + oy) * W + ox) * eps);
+#pragma unroll
+      for (int it = 0; it < E_IT; ++it) eo[it] = ld16(rb, eok[it], eoff[it] * 2);
+    };
+    // fragments: pixel r of tile rows 2 rw (+1); k-step j covers k = 32 j + 8 g
+    const int a_lane = (2 * rw * RS + r) * DROW;
+    int offA[KALIGN ? 1 : NSTEP];
+    if constexpr (!KALIGN) {
+#pragma unroll
+      for (int j = 0; j < NSTEP; ++j) {
+        const int k = 32 * j + 8 * g;
+        int tap = k / CK;
+        const int ci = k - tap * CK;
+        tap = tap < 9 ? tap : 8;   // padded k: zero weights, finite operand
+        offA[j] = a_lane + ((tap / 3) * RS + tap % 3) * DROW + ci * 2;
+      }
     }
+    const unsigned char* const pda = dyh + (KALIGN ? a_lane + g * 16 : 0);
+    const unsigned char* const pdb = wl + r * WROW + g * 16;
+    auto dgrad_tile = [&]() {
+      f32x4 acc[MT][NTL];
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int jn = 0; jn < NTL; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
+      {
+#pragma unroll
+        for (int j = 0; j < NSTEP; ++j) {
+          int ao;
+          if constexpr (KALIGN) {
+            const int k0 = 32 * j;
+            int tap = k0 / CK;
+            const int ci = k0 - tap * CK;
+            tap = tap < 9 ? tap : 8;
+            ao = ((tap / 3) * RS + tap % 3) * DROW + ci * 2;
+          } else {
+            ao = offA[j];
+          }
+          u32x4 fa[MT], fb[NTL];
+#pragma unroll
+          for (int i = 0; i < MT; ++i) fa[i] = *(const u32x4*)(pda + ao + i * RS * DROW);
+#pragma unroll
+          for (int jn = 0; jn < NTL; ++jn) fb[jn] = *(const u32x4*)(pdb + jn * 16 * WROW + j * 64);
+#pragma unroll
+          for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int jn = 0; jn < NTL; ++jn)
+              acc[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[i]),
+                                                                   __builtin_bit_cast(bf16x8, fb[jn]), acc[i][jn], 0,
+                                                                   0, 0);
+        }
+      }
+      // D[m = pixel][n = column]: lane rows g*4+e, column r
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int jn = 0; jn < NTL; ++jn)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) Ct[(rw * 32 + i * 16 + g * 4 + e) * CROWF + jn * 16 + r] = acc[i][jn][e];
+    };
+    auto epilogue = [&](int tt, const u32x4 (&eo)[E_IT]) {
+      int oy, ox, on;
+      origin(tt, oy, ox, on);
+      const int64_t opix0 = ((int64_t)on * H + oy) * W + ox;
+#pragma unroll
+      for (int it = 0; it < E_IT; ++it) {
+        const int u = rt + it * NR;
+        if (it + 1 == E_IT && u >= EU) continue;
+        const int c = ecol[it];
+        float v[VEC];
+        const float* src = Ct + (u / UPR) * CROWF + c;
+#pragma unroll
+        for (int q = 0; q < VEC; q += 4) {
+          const f32x4 t4 = *(const f32x4*)(src + q);
+          v[q] = t4[0]; v[q + 1] = t4[1]; v[q + 2] = t4[2]; v[q + 3] = t4[3];
+        }
+        if (eok[it]) {
+          float rv[VEC];
+          Unit16<bf16>::unpack(eo[it], rv);
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) v[q] += rv[q];
+        }
+        *(u32x4*)((bf16*)d.out + (opix0 + erel[it]) * d.out_ps +
+                  rdn_coff32(d.out_c0 + c, (int)d.out_ps, (int)d.out_pl)) = Unit16<bf16>::pack(v);
+      }
+    };
+
+    u32x4 lA[D_IT], gA[D_IT], lB[D_IT], gB[D_IT], eC[E_IT], eN[E_IT];
+    if (t < t_hi) {
+      load(t, lA, gA);
+      load_epi(t, eC);
+      store(lA, gA, true);
+      load(min(t + per, t_last), lA, gA);
+    }
+    __syncthreads();   // weights + first halos
+    auto step = [&](u32x4 (&lc)[D_IT], u32x4 (&gc)[D_IT], u32x4 (&ln)[D_IT], u32x4 (&gn)[D_IT],
+                    const u32x4 (&ec)[E_IT], u32x4 (&en)[E_IT]) -> bool {
+      const int t1 = t + per;
+      load(min(t + 2 * per, t_last), ln, gn);
+      load_epi(min(t1, t_last), en);
+      dgrad_tile();
+      __syncthreads();   // halos of t consumed, dX tile complete in Ct
+      store(lc, gc, t1 < t_hi);   // unconditional (past the range: a re-read of the last tile)
+      epilogue(t, ec);
+      __syncthreads();   // halos of t1 visible, Ct consumed
+      t = t1;
+      return t < t_hi;
+    };
+    if (t < t_hi)
+      while (step(lA, gA, lB, gB, eC, eN) && step(lB, gB, lA, gA, eN, eC)) {}
+
+    // dalpha / dbias partials of this split, fixed order
+    if (wg.part) {
+      float* red = (float*)(lds + Cfg::W_BYTES);   // the loop ended with a barrier
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) {
+        red[rt * VEC + k] = sa[k];
+        red[NR * VEC + rt * VEC + k] = sb[k];
+      }
+      __syncthreads();   // D waves only (W waves never pass a barrier after their loop)
+      if (rt < CK) {
+        const int cg = rt / VEC, k = rt % VEC;
+        float a = 0.f, b = 0.f;
+        for (int rr = 0; rr < NR / DU; ++rr) {
+          a += red[(rr * DU + cg) * VEC + k];
+          b += red[NR * VEC + (rr * DU + cg) * VEC + k];
+        }
+        if (rt < wg.mdim) {
+          wg.part[((int64_t)blockIdx.x * 2 + 0) * wg.mdim + rt] = a;
+          wg.part[((int64_t)blockIdx.x * 2 + 1) * wg.mdim + rt] = b;
+        }
+      }
+    }
+  } else {
+    // ================= W waves: X halo, wgrad
+    const int xupp = (wg.b_pl && wg.b_c0 % wg.b_ps == 0 && XU % (wg.b_ps / VEC) == 0) ? (int)(wg.b_ps / VEC) : XU;
+    int lrel[X_IT], llds[X_IT], uhp[X_IT];
 #pragma unroll
     for (int it = 0; it < X_IT; ++it) {
-      if (it + 1 == X_IT && tid + it * NT >= X_UNITS) continue;
-      *(u32x4*)(xh + xlds[it]) = xr[it];
+      const int u = rt + it * NR;
+      const int pln = u / (HW_ * xupp), rem = u - pln * (HW_ * xupp);
+      const bool ok = u < X_UNITS;
+      const int hp = ok ? rem / xupp : HW_, cu = ok ? pln * xupp + rem % xupp : 0;
+      const int hq = hp < HW_ ? hp : 0;
+      const int hy = hq / RS, hx = hq - hy * RS;
+      uhp[it] = hp;
+      lrel[it] = (hy * W + hx) * (int)wg.b_ps + rdn_coff32(wg.b_c0 + cu * VEC, (int)wg.b_ps, (int)wg.b_pl);
+      llds[it] = hq * XROW + cu * 16;
     }
-  };
-  // epilogue operand (residual, else the accumulated output) of a tile, one tile ahead
-  auto load_epi = [&](int oy, int ox, int on, u32x4 (&eo)[E_IT]) {
-    if (!has_res && !has_acc) return;
-    const int64_t opix0 = ((int64_t)on * H + oy) * W + ox;
+    auto load = [&](int tt, u32x4 (&lr)[X_IT]) {
+      int oy, ox, on;
+      origin(tt, oy, ox, on);
+      const int64_t hpix0 = ((int64_t)on * H + (oy - 1)) * W + (ox - 1);
+      const __amdgpu_buffer_rsrc_t rx = rsrc_of(XS + hpix0 * wg.b_ps);
 #pragma unroll
-    for (int it = 0; it < E_IT; ++it) {
-      if (it + 1 == E_IT && tid + it * NT >= EU) continue;
-      const int c = ecol[it];
-      const int64_t opix = opix0 + erel[it];
-      if (has_res) {
-        if (c < d.res_climit)
-          eo[it] = *(const u32x4*)((const bf16*)d.res + opix * d.res_ps +
-                                   rdn_coff32(d.res_c0 + c, (int)d.res_ps, (int)d.res_pl));
-      } else {
-        eo[it] = *(const u32x4*)((const bf16*)d.out + opix * d.out_ps +
-                                 rdn_coff32(d.out_c0 + c, (int)d.out_ps, (int)d.out_pl));
-      }
+      for (int it = 0; it < X_IT; ++it) lr[it] = ld16(rx, in_img(uhp[it], oy, ox), lrel[it] * 2);
+    };
+    auto store = [&](const u32x4 (&lr)[X_IT]) {
+#pragma unroll
+      for (int it = 0; it < X_IT; ++it)
+        if (uhp[it] < HW_) *(u32x4*)(xh + llds[it]) = lr[it];
+    };
+    // lane (g, q = r>>2, pp = r&3) supplies pixels {4g+q, 16+4g+q} of each 32-pixel
+    // k-step (tile rows 2ks, 2ks+1) and channels / columns 4pp..4pp+3
+    const int q4 = r >> 2, pp = r & 3;
+    const unsigned char* const pwa = dyh + (RS + 4 * g + q4 + 1) * DROW + 4 * pp * 2;   // interior (0, 4g+q)
+    const unsigned char* const pwb = xh + (4 * g + q4) * XROW;
+    int boff[NTW];
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      const int nt = rw + 4 * j;
+      const int c = nt < NT_ALL ? nt * 16 + 4 * pp : 0;
+      const int tp = c / BN, ci = c - (c / BN) * BN;
+      boff[j] = ((tp / 3) * RS + tp % 3) * XROW + ci * 2;
     }
-  };
-
-  // ---- fragment addressing (per lane, tile-invariant)
-  // dgrad A: pixel r of tile row `wave`; k-step j covers k = 32 j + 8 g
-  const int a_lane = (wave * RS + r) * DROW;
-  int offA[KALIGN ? 1 : NSTEP];
-  if constexpr (!KALIGN) {
-#pragma unroll
-    for (int j = 0; j < NSTEP; ++j) {
-      const int k = 32 * j + 8 * g;
-      int tap = k / CK;
-      const int ci = k - tap * CK;
-      tap = tap < 9 ? tap : 8;   // padded k: zero weights, finite operand
-      offA[j] = a_lane + ((tap / 3) * RS + tap % 3) * DROW + ci * 2;
-    }
-  }
-  const unsigned char* const pda = dyh + (KALIGN ? a_lane + g * 16 : 0);
-  const unsigned char* const pdb = wl + r * WROW + g * 16;
-  // wgrad: lane (g, q = r>>2, pp = r&3) supplies pixels {4g+q, 16+4g+q} of each
-  // 32-pixel k-step (tile rows 2ks, 2ks+1) and channels / columns 4pp..4pp+3
-  const int q4 = r >> 2, pp = r & 3;
-  const unsigned char* const pwa = dyh + (RS + 4 * g + q4 + 1) * DROW + 4 * pp * 2;   // interior (0, 4g+q)
-  const unsigned char* const pwb = xh + (4 * g + q4) * XROW;
-  int boff[NTW];
-#pragma unroll
-  for (int j = 0; j < NTW; ++j) {
-    const int nt = wave + 8 * j;
-    const int c = nt < NT_ALL ? nt * 16 + 4 * pp : 0;
-    const int tp = c / BN, ci = c - (c / BN) * BN;
-    boff[j] = ((tp / 3) * RS + tp % 3) * XROW + ci * 2;
-  }
-
-  f32x4 accW[MTW][NTW];
-#pragma unroll
-  for (int i = 0; i < MTW; ++i)
-#pragma unroll
-    for (int j = 0; j < NTW; ++j) accW[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  auto compute_tile = [&]() {
-    // input gradient of the tile: 16 pixels x BN columns per wave
-    f32x4 accD[NTL];
-#pragma unroll
-    for (int jn = 0; jn < NTL; ++jn) accD[jn] = f32x4{0.f, 0.f, 0.f, 0.f};
-    if (!(dbg & 1))
-#pragma unroll
-    for (int j = 0; j < NSTEP; ++j) {
-      int ao;
-      if constexpr (KALIGN) {
-        const int k0 = 32 * j;
-        int tap = k0 / CK;
-        const int ci = k0 - tap * CK;
-        tap = tap < 9 ? tap : 8;
-        ao = ((tap / 3) * RS + tap % 3) * DROW + ci * 2;
-      } else {
-        ao = offA[j];
-      }
-      const u32x4 af = *(const u32x4*)(pda + ao);
-#pragma unroll
-      for (int jn = 0; jn < NTL; ++jn) {
-        const u32x4 bfr = *(const u32x4*)(pdb + jn * 16 * WROW + j * 64);
-        accD[jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af),
-                                                           __builtin_bit_cast(bf16x8, bfr), accD[jn], 0, 0, 0);
-      }
-    }
-    // weight gradient: K = the tile's 128 pixels, 4 k-steps
-    if (!(dbg & 2))
-#pragma unroll
-    for (int ks = 0; ks < TH / 2; ++ks) {
-      bf16x8 af[MTW];
-#pragma unroll
-      for (int i = 0; i < MTW; ++i) {
-        const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, pwa + (2 * ks) * RS * DROW + i * 32));
-        const i16x4 hi =
-            __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, pwa + (2 * ks + 1) * RS * DROW + i * 32));
-        af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-      }
-#pragma unroll
-      for (int j = 0; j < NTW; ++j) {
-        if (wave + 8 * j >= NT_ALL) continue;   // wave-uniform
-        const unsigned char* b = pwb + boff[j] + (2 * ks) * RS * XROW;
-        const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, b));
-        const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, b + RS * XROW));
-        const bf16x8 bfr = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-#pragma unroll
-        for (int i = 0; i < MTW; ++i) accW[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, accW[i][j], 0, 0, 0);
-      }
-    }
-    // fp32 dX tile to LDS: D[m = pixel][n = column], lane rows g*4+e, column r
-#pragma unroll
-    for (int jn = 0; jn < NTL; ++jn)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) Ct[(wave * 16 + g * 4 + e) * CROWF + jn * 16 + r] = accD[jn][e];
-  };
-  auto epilogue = [&](int oy, int ox, int on, const u32x4 (&eo)[E_IT]) {
-    const int64_t opix0 = ((int64_t)on * H + oy) * W + ox;
-#pragma unroll
-    for (int it = 0; it < E_IT; ++it) {
-      const int u = tid + it * NT;
-      if (it + 1 == E_IT && u >= EU) continue;
-      const int c = ecol[it];
-      float v[VEC];
-      const float* src = Ct + (u / UPR) * CROWF + c;
-#pragma unroll
-      for (int q = 0; q < VEC; q += 4) {
-        const f32x4 t4 = *(const f32x4*)(src + q);
-        v[q] = t4[0]; v[q + 1] = t4[1]; v[q + 2] = t4[2]; v[q + 3] = t4[3];
-      }
-      const int64_t opix = opix0 + erel[it];
-      if ((has_res && c < d.res_climit) || has_acc) {
-        float rv[VEC];
-        Unit16<bf16>::unpack(eo[it], rv);
-#pragma unroll
-        for (int q = 0; q < VEC; ++q) v[q] += rv[q];
-      }
-      *(u32x4*)((bf16*)d.out + opix * d.out_ps + rdn_coff32(d.out_c0 + c, (int)d.out_ps, (int)d.out_pl)) =
-          Unit16<bf16>::pack(v);
-    }
-  };
-
-  // ---- the tile loop: LDS holds tile t; the next tile's loads are in flight
-  u32x4 dA[D_IT], gA[D_IT], xA[X_IT], eC[E_IT], eN[E_IT];
-  int y0 = 0, x0 = 0, nimg = 0;
-  if (t < t_hi) {
-    origin(t, y0, x0, nimg);
-    load_halos(y0, x0, nimg, dA, gA, xA);
-    load_epi(y0, x0, nimg, eC);
-    store_halos(dA, gA, xA);
-  }
-  __syncthreads();   // weights + first halos
-  while (t < t_hi) {
-    const int t1 = t + per;
-    int y1 = 0, x1 = 0, n1 = 0;
-    if (t1 < t_hi) {
-      origin(t1, y1, x1, n1);
-      load_epi(y1, x1, n1, eN);
-      load_halos(y1, x1, n1, dA, gA, xA);
-    }
-    compute_tile();
-    __syncthreads();   // halos consumed, dX tile complete in Ct
-    if (t1 < t_hi) store_halos(dA, gA, xA);
-    if (!(dbg & 4)) epilogue(y0, x0, nimg, eC);
-    __syncthreads();   // next halos visible, Ct consumed
-#pragma unroll
-    for (int it = 0; it < E_IT; ++it) eC[it] = eN[it];
-    t = t1; y0 = y1; x0 = x1; nimg = n1;
-  }
-
-  // ---- this block's split: weight-gradient slab (zero for a block without tiles)
-  const int ncol_all = 9 * wg.ndim;
-  float* __restrict__ ws = wg.ws + (int64_t)blockIdx.x * wg.mdim * ncol_all;
-#pragma unroll
-  for (int j = 0; j < NTW; ++j) {
-    const int nt = wave + 8 * j;
-    if (nt >= NT_ALL) continue;
-    const int c = nt * 16 + r;
-    const int tp = c / BN, ci = c - tp * BN;
-    const int col = tp * wg.ndim + ci;
+    f32x4 accW[MTW][NTW];
 #pragma unroll
     for (int i = 0; i < MTW; ++i)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int m = i * 16 + g * 4 + e;
-        if (m < wg.mdim) ws[(int64_t)m * ncol_all + col] = accW[i][j][e];
-      }
-  }
-  // ---- dalpha / dbias partials of this split, fixed order
-  if (wg.part) {
-    float* red = (float*)(lds + Cfg::W_BYTES);   // the loop ended with a barrier
+      for (int j = 0; j < NTW; ++j) accW[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto wgrad_tile = [&]() {
 #pragma unroll
-    for (int k = 0; k < VEC; ++k) {
-      red[tid * VEC + k] = sa[k];
-      red[NT * VEC + tid * VEC + k] = sb[k];
+      for (int ks = 0; ks < TH / 2; ++ks) {
+        bf16x8 af[MTW];
+#pragma unroll
+        for (int i = 0; i < MTW; ++i) {
+          const i16x4 lo =
+              __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, pwa + (2 * ks) * RS * DROW + i * 32));
+          const i16x4 hi =
+              __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, pwa + (2 * ks + 1) * RS * DROW + i * 32));
+          af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+#pragma unroll
+        for (int j = 0; j < NTW; ++j) {
+          if (rw + 4 * j >= NT_ALL) continue;   // wave-uniform
+          const unsigned char* b = pwb + boff[j] + (2 * ks) * RS * XROW;
+          const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, b));
+          const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, b + RS * XROW));
+          const bf16x8 bfr = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+          for (int i = 0; i < MTW; ++i)
+            accW[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, accW[i][j], 0, 0, 0);
+        }
+      }
+    };
+
+    if constexpr (DW2) {   // two tiles in flight: register sets alternate
+      u32x4 lA[X_IT], lB[X_IT];
+      if (t < t_hi) {
+        load(t, lA);
+        store(lA);
+        load(min(t + per, t_last), lA);
+      }
+      __syncthreads();   // weights + first halos
+      auto step = [&](u32x4 (&lc)[X_IT], u32x4 (&ln)[X_IT]) -> bool {
+        load(min(t + 2 * per, t_last), ln);
+        wgrad_tile();
+        __syncthreads();   // halos of t consumed
+        store(lc);
+        __syncthreads();   // halos of t1 visible
+        t += per;
+        return t < t_hi;
+      };
+      if (t < t_hi)
+        while (step(lA, lB) && step(lB, lA)) {}
+    } else {   // one tile in flight (the register budget of the widest shapes)
+      u32x4 lA[X_IT];
+      if (t < t_hi) {
+        load(t, lA);
+        store(lA);
+      }
+      __syncthreads();   // weights + first halos
+      while (t < t_hi) {
+        load(min(t + per, t_last), lA);
+        wgrad_tile();
+        __syncthreads();   // halos of t consumed
+        store(lA);
+        __syncthreads();   // halos of t1 visible
+        t += per;
+      }
     }
-    __syncthreads();
-    if (tid < CK) {
-      const int cg = tid / VEC, k = tid % VEC;
-      float a = 0.f, b = 0.f;
-      for (int rr = 0; rr < NT / DU; ++rr) {
-        a += red[(rr * DU + cg) * VEC + k];
-        b += red[NT * VEC + (rr * DU + cg) * VEC + k];
-      }
-      if (tid < wg.mdim) {
-        wg.part[((int64_t)blockIdx.x * 2 + 0) * wg.mdim + tid] = a;
-        wg.part[((int64_t)blockIdx.x * 2 + 1) * wg.mdim + tid] = b;
-      }
+
+    // this block's split of the weight gradient (zero slab for a block without tiles)
+    const int ncol_all = 9 * wg.ndim;
+    float* __restrict__ ws = wg.ws + (int64_t)blockIdx.x * wg.mdim * ncol_all;
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      const int nt = rw + 4 * j;
+      if (nt >= NT_ALL) continue;
+      const int c = nt * 16 + r;
+      const int tp = c / BN, ci = c - tp * BN;
+      const int col = tp * wg.ndim + ci;
+#pragma unroll
+      for (int i = 0; i < MTW; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int m = i * 16 + g * 4 + e;
+          if (m < wg.mdim) ws[(int64_t)m * ncol_all + col] = accW[i][j][e];
+        }
     }
   }
 }
@@ -470,6 +543,7 @@ bool dw_serves(const rdn_conv_desc* d, const rdn_wgrad_desc* wg) {
   if (d->dtype != RDN_BF16 || wg->dtype != RDN_BF16 || d->gather != RDN_G_CONV3 || wg->gather != RDN_G_CONV3) return false;
   if (!d->gate || !wg->a_gate || !d->gate_alpha || d->bn || d->bm) return false;
   if (d->flags & ~(RDN_EPI_RESID | RDN_EPI_ACCUM)) return false;
+  if ((d->flags & RDN_EPI_RESID) && (d->flags & RDN_EPI_ACCUM)) return false;
   if (d->h % TH || d->w % TW || d->n != wg->n || d->h != wg->h || d->w != wg->w) return false;
   if (d->cin != 16 && d->cin != 32) return false;
   if (d->ncols != d->cout || d->ncols % 16 || d->ncols < 32 || d->ncols > 80 || wg->ndim != d->ncols) return false;
@@ -512,12 +586,8 @@ int launch_dw(const rdn_conv_desc* d, const rdn_wgrad_desc* wg, hipStream_t st) 
       return RDN_E_ARG;
     }
     if (!wg->ws) { rdn_set_error("rdn_conv_dgrad_wgrad: null workspace"); return RDN_E_ARG; }
-    static const int dbg = [] {   // RDN_DW_DBG (diagnosis only, wrong results): 1 no dgrad MFMA,
-      const char* e = getenv("RDN_DW_DBG");   // 2 no wgrad MFMA, 4 no dX stores
-      return e ? atoi(e) : 0;
-    }();
     hipLaunchKernelGGL((conv3_dw_kernel<BN, CK>), dim3((unsigned)grid), dim3(NT), 0, st, *d, *wg, tiles_x, tiles_y,
-                       ntiles, dbg);
+                       ntiles);
     return rdn_check_launch("rdn_conv_dgrad_wgrad");
   }
 }
