@@ -381,18 +381,18 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
   } else {
     // ================= W waves: X halo, wgrad
     const int xupp = (wg.b_pl && wg.b_c0 % wg.b_ps == 0 && XU % (wg.b_ps / VEC) == 0) ? (int)(wg.b_ps / VEC) : XU;
-    int lrel[X_IT], llds[X_IT], uhp[X_IT];
+    // per unit: global offset and LDS offset (-1: padding unit; its halo pixel is
+    // llds / XROW, so no third array)
+    int lrel[X_IT], llds[X_IT];
 #pragma unroll
     for (int it = 0; it < X_IT; ++it) {
       const int u = rt + it * NR;
       const int pln = u / (HW_ * xupp), rem = u - pln * (HW_ * xupp);
       const bool ok = u < X_UNITS;
-      const int hp = ok ? rem / xupp : HW_, cu = ok ? pln * xupp + rem % xupp : 0;
-      const int hq = hp < HW_ ? hp : 0;
+      const int hq = ok ? rem / xupp : 0, cu = ok ? pln * xupp + rem % xupp : 0;
       const int hy = hq / RS, hx = hq - hy * RS;
-      uhp[it] = hp;
       lrel[it] = (hy * W + hx) * (int)wg.b_ps + rdn_coff32(wg.b_c0 + cu * VEC, (int)wg.b_ps, (int)wg.b_pl);
-      llds[it] = hq * XROW + cu * 16;
+      llds[it] = ok ? hq * XROW + cu * 16 : -1;
     }
     auto load = [&](int tt, u32x4 (&lr)[X_IT]) {
       int oy, ox, on;
@@ -400,26 +400,25 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       const int64_t hpix0 = ((int64_t)on * H + (oy - 1)) * W + (ox - 1);
       const __amdgpu_buffer_rsrc_t rx = rsrc_of(XS + hpix0 * wg.b_ps);
 #pragma unroll
-      for (int it = 0; it < X_IT; ++it) lr[it] = ld16(rx, in_img(uhp[it], oy, ox), lrel[it] * 2);
+      for (int it = 0; it < X_IT; ++it)
+        lr[it] = ld16(rx, in_img(llds[it] < 0 ? HW_ : llds[it] / XROW, oy, ox), lrel[it] * 2);
     };
     auto store = [&](const u32x4 (&lr)[X_IT]) {
 #pragma unroll
       for (int it = 0; it < X_IT; ++it)
-        if (uhp[it] < HW_) *(u32x4*)(xh + llds[it]) = lr[it];
+        if (llds[it] >= 0) *(u32x4*)(xh + llds[it]) = lr[it];
     };
     // lane (g, q = r>>2, pp = r&3) supplies pixels {4g+q, 16+4g+q} of each 32-pixel
     // k-step (tile rows 2ks, 2ks+1) and channels / columns 4pp..4pp+3
     const int q4 = r >> 2, pp = r & 3;
     const unsigned char* const pwa = dyh + (RS + 4 * g + q4 + 1) * DROW + 4 * pp * 2;   // interior (0, 4g+q)
     const unsigned char* const pwb = xh + (4 * g + q4) * XROW;
-    int boff[NTW];
-#pragma unroll
-    for (int j = 0; j < NTW; ++j) {
+    auto boff = [&](int j) {   // column offset of n-tile rw + 4 j (recomputed: registers)
       const int nt = rw + 4 * j;
       const int c = nt < NT_ALL ? nt * 16 + 4 * pp : 0;
       const int tp = c / BN, ci = c - (c / BN) * BN;
-      boff[j] = ((tp / 3) * RS + tp % 3) * XROW + ci * 2;
-    }
+      return ((tp / 3) * RS + tp % 3) * XROW + ci * 2;
+    };
     f32x4 accW[MTW][NTW];
 #pragma unroll
     for (int i = 0; i < MTW; ++i)
@@ -440,7 +439,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
 #pragma unroll
         for (int j = 0; j < NTW; ++j) {
           if (rw + 4 * j >= NT_ALL) continue;   // wave-uniform
-          const unsigned char* b = pwb + boff[j] + (2 * ks) * RS * XROW;
+          const unsigned char* b = pwb + boff(j) + (2 * ks) * RS * XROW;
           const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, b));
           const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, b + RS * XROW));
           const bf16x8 bfr = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));

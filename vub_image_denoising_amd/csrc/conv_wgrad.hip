@@ -350,8 +350,13 @@ extern "C" int rdn_wgrad_reduce(const float* ws, int32_t splits, int32_t mdim, i
   }
   const int64_t total = (int64_t)mdim * ndim * taps;
   if (ndim % 4 || ((uintptr_t)ws & 15)) { rdn_set_error("rdn_wgrad_reduce: ndim %% 4 / alignment"); return RDN_E_ARG; }
+  // split lanes per column quad: only as many as it takes to give the launch ~64k
+  // threads (one per lane of every SIMD); each lane then streams its splits with
+  // four loads in flight.  (Lanes for every split up to 16 -- the previous rule --
+  // left the wide level-2/3 reductions at one or two loads per thread: 0.7 TB/s.)
+  const int64_t quads = total / 4;
   int sl = 1;
-  while (sl < 16 && sl < splits) sl <<= 1;
+  while (sl < 16 && sl < splits && quads * sl < 65536) sl <<= 1;
   const int qpb = 256 / sl;
   int64_t blocks = (total / 4 + qpb - 1) / qpb;
   if (part && blocks < 2 * mdim) blocks = 2 * mdim;
