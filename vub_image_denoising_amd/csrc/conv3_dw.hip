@@ -72,22 +72,6 @@ struct DwCfg {
   static constexpr bool FITS = LDS <= LDS_MAX && D_BYTES + X_BYTES + CT_BYTES >= RED_BYTES;
 };
 
-// 16-byte load through a buffer descriptor on a wave-uniform base: a byte offset
-// past the descriptor's range (OOB) returns zeros -- halo padding without branches,
-// so the compiler's vmcnt waits stay exact (a predicated flat load became a branch
-// with a vmcnt(0) inside)
-constexpr int OOB = 0x7ffffff0;
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* base) {
-  const uint64_t a = (uint64_t)(uintptr_t)base;
-  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a), hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
-  return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | lo), 0, OOB, 0x00020000);
-}
-__device__ __forceinline__ u32x4 ld16(__amdgpu_buffer_rsrc_t rs, bool ok, int off_bytes) {
-  int o = ok ? off_bytes : OOB;
-  asm volatile("" : "+v"(o));   // opaque: keeps ONE load (hipcc otherwise splits it into two predicated ones)
-  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0));
-}
-
 template <int BN, int CK>
 __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wgrad_desc wg, int tiles_x, int tiles_y,
                                                          int ntiles) {
@@ -213,12 +197,12 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       int oy, ox, on;
       origin(tt, oy, ox, on);
       const int64_t hpix0 = ((int64_t)on * H + (oy - 1)) * W + (ox - 1);
-      const __amdgpu_buffer_rsrc_t rd = rsrc_of(DY + hpix0 * d.x_ps), rg = rsrc_of(PR + hpix0 * d.gate_ps);
+      const __amdgpu_buffer_rsrc_t rd = rdn_rsrc(DY + hpix0 * d.x_ps), rg = rdn_rsrc(PR + hpix0 * d.gate_ps);
 #pragma unroll
       for (int it = 0; it < D_IT; ++it) {
         const bool ok = in_img(uhp[it], oy, ox);
-        lr[it] = ld16(rd, ok, lrel[it] * 2);
-        gr[it] = ld16(rg, ok, grel[it] * 2);
+        lr[it] = rdn_ld16(rd, ok, lrel[it] * 2);
+        gr[it] = rdn_ld16(rg, ok, grel[it] * 2);
       }
     };
     // registers -> LDS with the PReLU-backward gate and the dalpha/dbias partials of
@@ -245,9 +229,9 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     auto load_epi = [&](int tt, u32x4 (&eo)[E_IT]) {
       int oy, ox, on;
       origin(tt, oy, ox, on);
-      const __amdgpu_buffer_rsrc_t rb = rsrc_of(ebase + (((int64_t)on * H + oy) * W + ox) * eps);
+      const __amdgpu_buffer_rsrc_t rb = rdn_rsrc(ebase + (((int64_t)on * H + oy) * W + ox) * eps);
 #pragma unroll
-      for (int it = 0; it < E_IT; ++it) eo[it] = ld16(rb, eok[it], eoff[it] * 2);
+      for (int it = 0; it < E_IT; ++it) eo[it] = rdn_ld16(rb, eok[it], eoff[it] * 2);
     };
     // fragments: pixel r of tile rows 2 rw (+1); k-step j covers k = 32 j + 8 g
     const int a_lane = (2 * rw * RS + r) * DROW;
@@ -398,10 +382,10 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       int oy, ox, on;
       origin(tt, oy, ox, on);
       const int64_t hpix0 = ((int64_t)on * H + (oy - 1)) * W + (ox - 1);
-      const __amdgpu_buffer_rsrc_t rx = rsrc_of(XS + hpix0 * wg.b_ps);
+      const __amdgpu_buffer_rsrc_t rx = rdn_rsrc(XS + hpix0 * wg.b_ps);
 #pragma unroll
       for (int it = 0; it < X_IT; ++it)
-        lr[it] = ld16(rx, in_img(llds[it] < 0 ? HW_ : llds[it] / XROW, oy, ox), lrel[it] * 2);
+        lr[it] = rdn_ld16(rx, in_img(llds[it] < 0 ? HW_ : llds[it] / XROW, oy, ox), lrel[it] * 2);
     };
     auto store = [&](const u32x4 (&lr)[X_IT]) {
 #pragma unroll

@@ -211,27 +211,22 @@ __global__ __launch_bounds__(NT, 2) void conv3_ws_kernel(rdn_conv_desc d, int ti
     ox = tx * TW;
     on = tt / tiles_y;
   };
+  // every load is issued unconditionally through a buffer descriptor (out-of-image
+  // units read zeros past its range): predicated flat loads became branches whose
+  // vmcnt(0) waits drained the next tile's loads
   auto load_halo = [&](int oy, int ox, int on, u32x4 (&hreg)[H_IT], u32x4 (&greg)[GH]) {
     const int64_t hpix0 = ((int64_t)on * H + (oy - 1)) * W + (ox - 1);   // halo pixel (0, 0)
-    const bf16* const xb = X + hpix0 * d.x_ps;
-    const bf16* const gb = GATE ? G + hpix0 * d.gate_ps : nullptr;
-    const bool interior = oy >= 1 && oy + TH + 1 <= H && ox >= 1 && ox + TW + 1 <= W;
+    const __amdgpu_buffer_rsrc_t rx = rdn_rsrc(X + hpix0 * d.x_ps);
+    const __amdgpu_buffer_rsrc_t rg = rdn_rsrc(GATE ? G + hpix0 * d.gate_ps : X);
 #pragma unroll
     for (int it = 0; it < H_IT; ++it) {
       const int u = tid + it * NT;
-      bool ok = (it + 1 < H_IT) || u < H_UNITS;
-      if (!interior) {
-        const int hp = hlds[it] / HROW;   // this unit's halo pixel (pixel- or plane-major order)
-        const int hy = hp / (TW + 2), hx = hp - hy * (TW + 2);
-        ok = ok && (unsigned)(oy - 1 + hy) < (unsigned)H && (unsigned)(ox - 1 + hx) < (unsigned)W;
-      }
-      u32x4 v = {0u, 0u, 0u, 0u}, gv = {0u, 0u, 0u, 0u};
-      if (ok) {
-        v = *(const u32x4*)(xb + hrel[it]);
-        if constexpr (GATE) gv = *(const u32x4*)(gb + grel[it]);
-      }
-      hreg[it] = v;
-      if constexpr (GATE) greg[it] = gv;
+      const int hp = hlds[it] / HROW;   // this unit's halo pixel (pixel- or plane-major order)
+      const int hy = hp / (TW + 2), hx = hp - hy * (TW + 2);
+      const bool ok = ((it + 1 < H_IT) || u < H_UNITS) & ((unsigned)(oy - 1 + hy) < (unsigned)H) &
+                      ((unsigned)(ox - 1 + hx) < (unsigned)W);
+      hreg[it] = rdn_ld16(rx, ok, hrel[it] * 2);
+      if constexpr (GATE) greg[it] = rdn_ld16(rg, ok, grel[it] * 2);
     }
   };
   auto store_halo = [&](const u32x4 (&hreg)[H_IT], const u32x4 (&greg)[GH]) {
@@ -259,16 +254,17 @@ __global__ __launch_bounds__(NT, 2) void conv3_ws_kernel(rdn_conv_desc d, int ti
   u32x4 eop[PF ? E_IT : 1];
   auto load_epi = [&](int oy, int ox, int on) {
     if constexpr (!PF) return;
-    if (!(pf_res || pf_acc) || oy + TH > H || ox + TW > W) return;
+    if (!(pf_res || pf_acc)) return;   // launch-uniform
+    const bool full = oy + TH <= H && ox + TW <= W;   // other tiles take the generic epilogue
     const int64_t opix0 = ((int64_t)on * H + oy) * W + ox;
-    const bf16* const base = pf_res ? (const bf16*)d.res + opix0 * d.res_ps : (const bf16*)d.out + opix0 * d.out_ps;
     const int ps = pf_res ? d.res_ps : d.out_ps;
+    const __amdgpu_buffer_rsrc_t rb =
+        rdn_rsrc(pf_res ? (const bf16*)d.res + opix0 * d.res_ps : (const bf16*)d.out + opix0 * d.out_ps);
 #pragma unroll
     for (int it = 0; it < E_IT; ++it) {
-      if (it + 1 == E_IT && tid + it * NT >= EU) continue;
       const int c = col_of(it);
-      if (c < (pf_res ? d.res_climit : d.ncols))
-        eop[it] = *(const u32x4*)(base + erel[it] * ps + (pf_res ? off_res(c) : off_out(c)));
+      const bool ok = full && ((it + 1 < E_IT) || tid + it * NT < EU) && c < (pf_res ? d.res_climit : d.ncols);
+      eop[it] = rdn_ld16(rb, ok, (erel[it] * ps + (pf_res ? off_res(c) : off_out(c))) * 2);
     }
   };
 
@@ -372,6 +368,10 @@ __global__ __launch_bounds__(NT, 2) void conv3_ws_kernel(rdn_conv_desc d, int ti
 
   };
 
+  // Loads of a tile past the block's range re-read its last tile: every load is
+  // issued on every path, so the compiler's vmcnt waits count exactly (a uniform
+  // branch around them left it draining the other register set).
+  const int t_last = t_hi - 1;
   int y0, x0, nimg;
   origin(t, y0, x0, nimg);
   load_halo(y0, x0, nimg, hA, gA);
@@ -381,26 +381,17 @@ __global__ __launch_bounds__(NT, 2) void conv3_ws_kernel(rdn_conv_desc d, int ti
   // invariant at a step: LDS holds tile t; the next tile's loads (t1) are in flight
   // in one register set (DEPTH 2) and the tile after (t2) is issued into the other
   int t1 = t + per, y1 = 0, x1 = 0, n1 = 0;
-  if constexpr (DEPTH == 2) {
-    if (t1 < t_hi) {
-      origin(t1, y1, x1, n1);
-      load_halo(y1, x1, n1, hA, gA);
-    }
-  }
+  origin(min(t1, t_last), y1, x1, n1);
+  if constexpr (DEPTH == 2) load_halo(y1, x1, n1, hA, gA);
   auto step = [&](u32x4 (&hn)[H_IT], u32x4 (&gn)[GH], u32x4 (&hf)[H_IT], u32x4 (&gf)[GH]) -> bool {
     // hn/gn: the next tile's registers; hf/gf: free for the tile after it
     int y2 = 0, x2 = 0, n2 = 0;
     const int t2 = t1 + per;
+    origin(min(t2, t_last), y2, x2, n2);
     if constexpr (DEPTH == 2) {
-      if (t2 < t_hi) {
-        origin(t2, y2, x2, n2);
-        load_halo(y2, x2, n2, hf, gf);   // in flight during the next TWO tiles
-      }
+      load_halo(y2, x2, n2, hf, gf);   // in flight during the next TWO tiles
     } else {
-      if (t1 < t_hi) {
-        origin(t1, y1, x1, n1);
-        load_halo(y1, x1, n1, hn, gn);   // in flight during this tile's MFMAs and epilogue
-      }
+      load_halo(y1, x1, n1, hn, gn);   // in flight during this tile's MFMAs and epilogue
     }
     compute_tile(y0, x0, nimg);
     if (t1 >= t_hi) return false;
@@ -476,6 +467,16 @@ int launch_ws(const rdn_conv_desc* d, hipStream_t st) {
     const int64_t nt = (int64_t)d->n * tiles_x * tiles_y;
     if (nt >= (1ll << 31)) return 1;
     const int ntiles = (int)nt;
+    {   // byte offsets of the tile-relative buffer loads stay below RDN_OOB
+      const int64_t span = (int64_t)(TH + 2) * d->w;
+      auto fits = [&](int64_t ps, int64_t pl, int c_hi) {
+        return 2 * (span * ps + rdn_coff(c_hi, ps, pl)) < (int64_t)RDN_OOB - 16;
+      };
+      if (!fits(d->x_ps, d->x_pl, d->x_c0 + d->cin) || (d->gate && !fits(d->gate_ps, d->gate_pl, d->cin)) ||
+          ((d->flags & RDN_EPI_RESID) && d->res && !fits(d->res_ps, d->res_pl, d->res_c0 + d->ncols)) ||
+          (d->out && !fits(d->out_ps, d->out_pl, d->out_c0 + d->ncols)))
+        return 1;
+    }
     int dev = 0, cus = 256;
     (void)hipGetDevice(&dev);
     static int cached_cus = 0;

@@ -81,6 +81,22 @@ __device__ __forceinline__ int xcd_remap(int b, int nb) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
 }
 
+// 16-byte load through a buffer descriptor on a wave-uniform base: a byte offset
+// past the descriptor's range (OOB) returns zeros -- halo padding without branches,
+// so the compiler's vmcnt waits stay exact (a predicated flat load became a branch
+// with a vmcnt(0) inside)
+constexpr int RDN_OOB = 0x7ffffff0;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rdn_rsrc(const void* base) {
+  const uint64_t a = (uint64_t)(uintptr_t)base;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a), hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | lo), 0, RDN_OOB, 0x00020000);
+}
+__device__ __forceinline__ u32x4 rdn_ld16(__amdgpu_buffer_rsrc_t rs, bool ok, int off_bytes) {
+  int o = ok ? off_bytes : RDN_OOB;
+  asm volatile("" : "+v"(o));   // opaque: keeps ONE load (hipcc otherwise splits it into two predicated ones)
+  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0));
+}
+
 // Fast unsigned division by a runtime-invariant divisor (n < 2^31).
 struct FastDiv {
   uint32_t d, m, s;
