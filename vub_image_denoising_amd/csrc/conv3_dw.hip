@@ -64,8 +64,7 @@ struct DwCfg {
   static constexpr int XROW = c3::HaloRow<BN * 2>::V;   // X halo row stride
   static constexpr int D_BYTES = (HW_ * DROW + 15) / 16 * 16;
   static constexpr int X_BYTES = (HW_ * XROW + 15) / 16 * 16;
-  static constexpr int CROWF = BN + 4;                  // epilogue fp32 row (floats)
-  static constexpr int CT_BYTES = BM * CROWF * 4;
+  static constexpr int CT_BYTES = 0;                    // dX leaves from the accumulators
   static constexpr int RED_BYTES = 2 * 256 * 8 * 4;     // dalpha/dbias partial reduction (aliases)
   static constexpr int AL_BYTES = (CK * 4 + 15) / 16 * 16;   // gate slopes
   static constexpr int LDS = W_BYTES + D_BYTES + X_BYTES + CT_BYTES + AL_BYTES;
@@ -78,7 +77,6 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
   using Cfg = DwCfg<BN, CK>;
   constexpr int VEC = 8;
   constexpr int KC = Cfg::KC, NSTEP = Cfg::NSTEP, WROW = Cfg::WROW, DROW = Cfg::DROW, XROW = Cfg::XROW;
-  constexpr int CROWF = Cfg::CROWF;
   constexpr int NR = 256;                               // threads per role
   constexpr int MT = 2;                                 // dgrad: 2 x 16 pixels per D wave
   constexpr int NTL = BN / 16;                          // dgrad n-tiles
@@ -88,7 +86,6 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
   constexpr int MTW = CK / 16;                          // wgrad m-tiles
   constexpr int NT_ALL = 9 * BN / 16;                   // wgrad n-tiles
   constexpr int NTW = (NT_ALL + 3) / 4;                 // per W wave (n-tile = wave + 4 j)
-  constexpr int UPR = BN / VEC, EU = BM * UPR, E_IT = (EU + NR - 1) / NR;
   constexpr bool KALIGN = CK % 32 == 0;                 // a dgrad k-step never straddles a tap
   constexpr int RS = (TW + 2);                          // halo pixels per halo row
   static_assert(NR % DU == 0, "fixed dY channel group per thread");
@@ -102,7 +99,6 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
   unsigned char* const wl = lds;
   unsigned char* const dyh = lds + Cfg::W_BYTES;
   unsigned char* const xh = dyh + Cfg::D_BYTES;
-  float* const Ct = (float*)(xh + Cfg::X_BYTES);
   float* const alds = (float*)(xh + Cfg::X_BYTES + Cfg::CT_BYTES);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -176,22 +172,23 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       sa[q] = 0.f;
       sb[q] = 0.f;
     }
-    // epilogue units (dX): pixel offset in the tile + channel; the operand is the
-    // residual (channels < res_climit) or the accumulated output
-    int erel[E_IT], ecol[E_IT], eoff[E_IT];
-    bool eok[E_IT];
+    // dX epilogue straight from the accumulators: the dgrad MFMA runs with swapped
+    // operands (A = weights, B = dY), so a lane holds 4 consecutive input channels
+    // jn*16 + 4g .. +3 of pixel (tile row 2 rw + i, column r) -- one 8-byte store per
+    // (i, jn), no fp32 tile in LDS.  The operand: residual (channels < res_climit)
+    // or the accumulated output, prefetched one tile ahead.
     const bool has_res = flags & RDN_EPI_RESID, has_acc = flags & RDN_EPI_ACCUM;
     const bf16* const ebase = has_res ? (const bf16*)d.res : (const bf16*)d.out;
     const int eps = has_res ? (int)d.res_ps : (int)d.out_ps;
+    int coff_e[NTL], coff_o[NTL];
+    bool eok[NTL];
 #pragma unroll
-    for (int it = 0; it < E_IT; ++it) {
-      const int u = rt + it * NR;
-      const int px = u / UPR;
-      erel[it] = (px / TW) * W + px % TW;
-      const int c = ecol[it] = (u - px * UPR) * VEC;
-      eok[it] = (u < EU) && (has_res ? c < d.res_climit : has_acc);
-      eoff[it] = erel[it] * eps + (has_res ? rdn_coff32(d.res_c0 + c, (int)d.res_ps, (int)d.res_pl)
-                                           : rdn_coff32(d.out_c0 + c, (int)d.out_ps, (int)d.out_pl));
+    for (int jn = 0; jn < NTL; ++jn) {
+      const int c = jn * 16 + 4 * g;
+      eok[jn] = has_res ? c < d.res_climit : has_acc;
+      coff_e[jn] = has_res ? rdn_coff32(d.res_c0 + c, (int)d.res_ps, (int)d.res_pl)
+                           : rdn_coff32(d.out_c0 + c, (int)d.out_ps, (int)d.out_pl);
+      coff_o[jn] = rdn_coff32(d.out_c0 + c, (int)d.out_ps, (int)d.out_pl);
     }
     auto load = [&](int tt, u32x4 (&lr)[D_IT], u32x4 (&gr)[D_IT]) {
       int oy, ox, on;
@@ -226,12 +223,15 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
         *(u32x4*)(dyh + llds[it]) = Unit16<bf16>::pack(dy);
       }
     };
-    auto load_epi = [&](int tt, u32x4 (&eo)[E_IT]) {
+    auto load_epi = [&](int tt, u32x2 (&eo)[MT][NTL]) {
       int oy, ox, on;
       origin(tt, oy, ox, on);
       const __amdgpu_buffer_rsrc_t rb = rdn_rsrc(ebase + (((int64_t)on * H + oy) * W + ox) * eps);
 #pragma unroll
-      for (int it = 0; it < E_IT; ++it) eo[it] = rdn_ld16(rb, eok[it], eoff[it] * 2);
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int jn = 0; jn < NTL; ++jn)
+          eo[i][jn] = rdn_ld8(rb, eok[jn], (((2 * rw + i) * W + r) * eps + coff_e[jn]) * 2);
     };
     // fragments: pixel r of tile rows 2 rw (+1); k-step j covers k = 32 j + 8 g
     const int a_lane = (2 * rw * RS + r) * DROW;
@@ -248,75 +248,55 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     }
     const unsigned char* const pda = dyh + (KALIGN ? a_lane + g * 16 : 0);
     const unsigned char* const pdb = wl + r * WROW + g * 16;
-    auto dgrad_tile = [&]() {
+    auto dgrad_tile = [&](int tt, const u32x2 (&eo)[MT][NTL]) {
       f32x4 acc[MT][NTL];
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int jn = 0; jn < NTL; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
-      {
 #pragma unroll
-        for (int j = 0; j < NSTEP; ++j) {
-          int ao;
-          if constexpr (KALIGN) {
-            const int k0 = 32 * j;
-            int tap = k0 / CK;
-            const int ci = k0 - tap * CK;
-            tap = tap < 9 ? tap : 8;
-            ao = ((tap / 3) * RS + tap % 3) * DROW + ci * 2;
-          } else {
-            ao = offA[j];
-          }
-          u32x4 fa[MT], fb[NTL];
-#pragma unroll
-          for (int i = 0; i < MT; ++i) fa[i] = *(const u32x4*)(pda + ao + i * RS * DROW);
-#pragma unroll
-          for (int jn = 0; jn < NTL; ++jn) fb[jn] = *(const u32x4*)(pdb + jn * 16 * WROW + j * 64);
-#pragma unroll
-          for (int i = 0; i < MT; ++i)
-#pragma unroll
-            for (int jn = 0; jn < NTL; ++jn)
-              acc[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[i]),
-                                                                   __builtin_bit_cast(bf16x8, fb[jn]), acc[i][jn], 0,
-                                                                   0, 0);
+      for (int j = 0; j < NSTEP; ++j) {
+        int ao;
+        if constexpr (KALIGN) {
+          const int k0 = 32 * j;
+          int tap = k0 / CK;
+          const int ci = k0 - tap * CK;
+          tap = tap < 9 ? tap : 8;
+          ao = ((tap / 3) * RS + tap % 3) * DROW + ci * 2;
+        } else {
+          ao = offA[j];
         }
+        u32x4 fa[MT], fb[NTL];
+#pragma unroll
+        for (int i = 0; i < MT; ++i) fa[i] = *(const u32x4*)(pda + ao + i * RS * DROW);
+#pragma unroll
+        for (int jn = 0; jn < NTL; ++jn) fb[jn] = *(const u32x4*)(pdb + jn * 16 * WROW + j * 64);
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+          for (int jn = 0; jn < NTL; ++jn)   // D^T[m = column][n = pixel]
+            acc[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fb[jn]),
+                                                                 __builtin_bit_cast(bf16x8, fa[i]), acc[i][jn], 0,
+                                                                 0, 0);
       }
-      // D[m = pixel][n = column]: lane rows g*4+e, column r
+      int oy, ox, on;
+      origin(tt, oy, ox, on);
+      bf16* const ob = (bf16*)d.out + (((int64_t)on * H + oy) * W + ox) * d.out_ps;
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
-        for (int jn = 0; jn < NTL; ++jn)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) Ct[(rw * 32 + i * 16 + g * 4 + e) * CROWF + jn * 16 + r] = acc[i][jn][e];
-    };
-    auto epilogue = [&](int tt, const u32x4 (&eo)[E_IT]) {
-      int oy, ox, on;
-      origin(tt, oy, ox, on);
-      const int64_t opix0 = ((int64_t)on * H + oy) * W + ox;
-#pragma unroll
-      for (int it = 0; it < E_IT; ++it) {
-        const int u = rt + it * NR;
-        if (it + 1 == E_IT && u >= EU) continue;
-        const int c = ecol[it];
-        float v[VEC];
-        const float* src = Ct + (u / UPR) * CROWF + c;
-#pragma unroll
-        for (int q = 0; q < VEC; q += 4) {
-          const f32x4 t4 = *(const f32x4*)(src + q);
-          v[q] = t4[0]; v[q + 1] = t4[1]; v[q + 2] = t4[2]; v[q + 3] = t4[3];
+        for (int jn = 0; jn < NTL; ++jn) {
+          float v[4] = {acc[i][jn][0], acc[i][jn][1], acc[i][jn][2], acc[i][jn][3]};
+          if (eok[jn]) {
+            v[0] += bf16lo(eo[i][jn][0]); v[1] += bf16hi(eo[i][jn][0]);
+            v[2] += bf16lo(eo[i][jn][1]); v[3] += bf16hi(eo[i][jn][1]);
+          }
+          *(u32x2*)(ob + ((2 * rw + i) * W + r) * (int)d.out_ps + coff_o[jn]) = rdn_pack4(v);
         }
-        if (eok[it]) {
-          float rv[VEC];
-          Unit16<bf16>::unpack(eo[it], rv);
-#pragma unroll
-          for (int q = 0; q < VEC; ++q) v[q] += rv[q];
-        }
-        *(u32x4*)((bf16*)d.out + (opix0 + erel[it]) * d.out_ps +
-                  rdn_coff32(d.out_c0 + c, (int)d.out_ps, (int)d.out_pl)) = Unit16<bf16>::pack(v);
-      }
     };
 
-    u32x4 lA[D_IT], gA[D_IT], lB[D_IT], gB[D_IT], eC[E_IT], eN[E_IT];
+    u32x4 lA[D_IT], gA[D_IT], lB[D_IT], gB[D_IT];
+    u32x2 eC[MT][NTL], eN[MT][NTL];
     if (t < t_hi) {
       load(t, lA, gA);
       load_epi(t, eC);
@@ -325,15 +305,14 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     }
     __syncthreads();   // weights + first halos
     auto step = [&](u32x4 (&lc)[D_IT], u32x4 (&gc)[D_IT], u32x4 (&ln)[D_IT], u32x4 (&gn)[D_IT],
-                    const u32x4 (&ec)[E_IT], u32x4 (&en)[E_IT]) -> bool {
+                    const u32x2 (&ec)[MT][NTL], u32x2 (&en)[MT][NTL]) -> bool {
       const int t1 = t + per;
       load(min(t + 2 * per, t_last), ln, gn);
       load_epi(min(t1, t_last), en);
-      dgrad_tile();
-      __syncthreads();   // halos of t consumed, dX tile complete in Ct
+      dgrad_tile(t, ec);   // MFMAs + dX stores
+      __syncthreads();   // halos of t consumed
       store(lc, gc, t1 < t_hi);   // unconditional (past the range: a re-read of the last tile)
-      epilogue(t, ec);
-      __syncthreads();   // halos of t1 visible, Ct consumed
+      __syncthreads();   // halos of t1 visible
       t = t1;
       return t < t_hi;
     };

@@ -9,6 +9,7 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) short i16x4;
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
 typedef __bf16 bf16;
 
 #define RDN_LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
@@ -95,6 +96,23 @@ __device__ __forceinline__ u32x4 rdn_ld16(__amdgpu_buffer_rsrc_t rs, bool ok, in
   int o = ok ? off_bytes : RDN_OOB;
   asm volatile("" : "+v"(o));   // opaque: keeps ONE load (hipcc otherwise splits it into two predicated ones)
   return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0));
+}
+
+__device__ __forceinline__ u32x2 rdn_ld8(__amdgpu_buffer_rsrc_t rs, bool ok, int off_bytes) {
+  int o = ok ? off_bytes : RDN_OOB;
+  asm volatile("" : "+v"(o));
+  return __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(rs, o, 0, 0));
+}
+// 4 floats -> 4 bf16 (round to nearest even), as Unit16<bf16>::pack
+__device__ __forceinline__ u32x2 rdn_pack4(const float* f) {
+  u32x2 u;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const unsigned short lo = __builtin_bit_cast(unsigned short, (bf16)f[2 * i]);
+    const unsigned short hi = __builtin_bit_cast(unsigned short, (bf16)f[2 * i + 1]);
+    u[i] = (unsigned int)lo | ((unsigned int)hi << 16);
+  }
+  return u;
 }
 
 // Fast unsigned division by a runtime-invariant divisor (n < 2^31).
