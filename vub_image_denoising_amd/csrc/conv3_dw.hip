@@ -67,7 +67,14 @@ struct DwCfg {
   static constexpr int CT_BYTES = 0;                    // dX leaves from the accumulators
   static constexpr int RED_BYTES = 2 * 256 * 8 * 4;     // dalpha/dbias partial reduction (aliases)
   static constexpr int AL_BYTES = (CK * 4 + 15) / 16 * 16;   // gate slopes
-  static constexpr int LDS = W_BYTES + D_BYTES + X_BYTES + CT_BYTES + AL_BYTES;
+  // W waves keep two X halos in flight in registers where the budget allows it
+  // (accumulators MTW x NTW x 4 + two X_IT sets within 256 VGPRs at 2 waves/SIMD);
+  // otherwise ONE register set and two X halo buffers in LDS
+  static constexpr int X_IT = (HW_ * (BN / 8) + 255) / 256;
+  static constexpr int NTW = (9 * BN / 16 + 3) / 4;
+  static constexpr bool DW2 = (CK / 16) * NTW * 4 + 2 * X_IT * 4 <= 112;
+  static constexpr int XB = DW2 ? 1 : 2;
+  static constexpr int LDS = W_BYTES + D_BYTES + XB * X_BYTES + CT_BYTES + AL_BYTES;
   static constexpr bool FITS = LDS <= LDS_MAX && D_BYTES + X_BYTES + CT_BYTES >= RED_BYTES;
 };
 
@@ -91,15 +98,14 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
   static_assert(NR % DU == 0, "fixed dY channel group per thread");
   static_assert(BN % 16 == 0 && CK % 16 == 0, "16-wide MFMA tiles");
   static_assert(Cfg::FITS, "LDS");
-  // W waves keep two X halos in flight where the registers allow it (accumulators
-  // MTW x NTW x 4 + two X_IT sets within the 256-VGPR budget of 2 waves / SIMD)
-  constexpr bool DW2 = MTW * NTW * 4 + 2 * X_IT * 4 <= 112;
+  constexpr bool DW2 = Cfg::DW2;
+  static_assert(Cfg::X_IT == X_IT && Cfg::NTW == NTW, "cfg");
 
   __shared__ __attribute__((aligned(16))) unsigned char lds[Cfg::LDS];
   unsigned char* const wl = lds;
   unsigned char* const dyh = lds + Cfg::W_BYTES;
   unsigned char* const xh = dyh + Cfg::D_BYTES;
-  float* const alds = (float*)(xh + Cfg::X_BYTES + Cfg::CT_BYTES);
+  float* const alds = (float*)(xh + Cfg::XB * Cfg::X_BYTES + Cfg::CT_BYTES);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const bool dwave = wave < 4;                          // role (wave-uniform)
@@ -366,10 +372,10 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       for (int it = 0; it < X_IT; ++it)
         lr[it] = rdn_ld16(rx, in_img(llds[it] < 0 ? HW_ : llds[it] / XROW, oy, ox), lrel[it] * 2);
     };
-    auto store = [&](const u32x4 (&lr)[X_IT]) {
+    auto store = [&](const u32x4 (&lr)[X_IT], int xoff) {
 #pragma unroll
       for (int it = 0; it < X_IT; ++it)
-        if (llds[it] >= 0) *(u32x4*)(xh + llds[it]) = lr[it];
+        if (llds[it] >= 0) *(u32x4*)(xh + xoff + llds[it]) = lr[it];
     };
     // lane (g, q = r>>2, pp = r&3) supplies pixels {4g+q, 16+4g+q} of each 32-pixel
     // k-step (tile rows 2ks, 2ks+1) and channels / columns 4pp..4pp+3
@@ -387,9 +393,10 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     for (int i = 0; i < MTW; ++i)
 #pragma unroll
       for (int j = 0; j < NTW; ++j) accW[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    auto wgrad_tile = [&]() {
+    auto wgrad_tile = [&](int xoff) {
 #pragma unroll
       for (int ks = 0; ks < TH / 2; ++ks) {
+        __builtin_amdgcn_sched_barrier(0);   // k-steps stay apart: fragment registers of one at a time
         bf16x8 af[MTW];
 #pragma unroll
         for (int i = 0; i < MTW; ++i) {
@@ -402,7 +409,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
 #pragma unroll
         for (int j = 0; j < NTW; ++j) {
           if (rw + 4 * j >= NT_ALL) continue;   // wave-uniform
-          const unsigned char* b = pwb + boff(j) + (2 * ks) * RS * XROW;
+          const unsigned char* b = pwb + xoff + boff(j) + (2 * ks) * RS * XROW;
           const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, b));
           const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, b + RS * XROW));
           const bf16x8 bfr = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
@@ -417,35 +424,41 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       u32x4 lA[X_IT], lB[X_IT];
       if (t < t_hi) {
         load(t, lA);
-        store(lA);
+        store(lA, 0);
         load(min(t + per, t_last), lA);
       }
       __syncthreads();   // weights + first halos
       auto step = [&](u32x4 (&lc)[X_IT], u32x4 (&ln)[X_IT]) -> bool {
         load(min(t + 2 * per, t_last), ln);
-        wgrad_tile();
+        wgrad_tile(0);
         __syncthreads();   // halos of t consumed
-        store(lc);
+        store(lc, 0);
         __syncthreads();   // halos of t1 visible
         t += per;
         return t < t_hi;
       };
       if (t < t_hi)
         while (step(lA, lB) && step(lB, lA)) {}
-    } else {   // one tile in flight (the register budget of the widest shapes)
+    } else {
+      // one register set, two X halo buffers: at the top of step k the set holds tile
+      // k+1 (issued a whole step earlier); it goes to buffer (k+1)&1 -- free since
+      // step k-1's MFMAs -- and takes tile k+2 while tile k computes from buffer k&1
       u32x4 lA[X_IT];
       if (t < t_hi) {
         load(t, lA);
-        store(lA);
+        store(lA, 0);
+        load(min(t + per, t_last), lA);
       }
       __syncthreads();   // weights + first halos
+      int k = 0;
       while (t < t_hi) {
-        load(min(t + per, t_last), lA);
-        wgrad_tile();
-        __syncthreads();   // halos of t consumed
-        store(lA);
-        __syncthreads();   // halos of t1 visible
+        store(lA, ((k + 1) & 1) * Cfg::X_BYTES);   // tile t + per (a re-read past the range)
+        load(min(t + 2 * per, t_last), lA);
+        wgrad_tile((k & 1) * Cfg::X_BYTES);
+        __syncthreads();   // halos of t consumed; X of t + per visible
+        __syncthreads();   // (the D waves' dY halo of t + per)
         t += per;
+        ++k;
       }
     }
 
