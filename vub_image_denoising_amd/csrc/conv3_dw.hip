@@ -73,8 +73,12 @@ struct DwCfg {
   static constexpr int X_IT = (HW_ * (BN / 8) + 255) / 256;
   static constexpr int NTW = (9 * BN / 16 + 3) / 4;
   static constexpr bool DW2 = (CK / 16) * NTW * 4 + 2 * X_IT * 4 <= 112;
-  static constexpr int XB = DW2 ? 1 : 2;
-  static constexpr int LDS = W_BYTES + D_BYTES + XB * X_BYTES + CT_BYTES + AL_BYTES;
+  static constexpr int BASE = W_BYTES + D_BYTES + CT_BYTES + AL_BYTES;
+  // X halo buffers in LDS: 2 for the LDS double buffer, 1 where it would not fit
+  // (96 columns were tried: <96,32> spills 128 B in the W loop, so they stay on the
+  // separate kernels)
+  static constexpr int XB = DW2 ? 1 : (BASE + 2 * X_BYTES <= LDS_MAX ? 2 : 1);
+  static constexpr int LDS = BASE + XB * X_BYTES;
   static constexpr bool FITS = LDS <= LDS_MAX && D_BYTES + X_BYTES + CT_BYTES >= RED_BYTES;
 };
 
@@ -439,7 +443,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       };
       if (t < t_hi)
         while (step(lA, lB) && step(lB, lA)) {}
-    } else {
+    } else if constexpr (Cfg::XB == 2) {
       // one register set, two X halo buffers: at the top of step k the set holds tile
       // k+1 (issued a whole step earlier); it goes to buffer (k+1)&1 -- free since
       // step k-1's MFMAs -- and takes tile k+2 while tile k computes from buffer k&1
@@ -459,6 +463,21 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
         __syncthreads();   // (the D waves' dY halo of t + per)
         t += per;
         ++k;
+      }
+    } else {   // one tile of X in flight (96 columns: neither budget holds two)
+      u32x4 lA[X_IT];
+      if (t < t_hi) {
+        load(t, lA);
+        store(lA, 0);
+      }
+      __syncthreads();   // weights + first halos
+      while (t < t_hi) {
+        load(min(t + per, t_last), lA);
+        wgrad_tile(0);
+        __syncthreads();   // halos of t consumed
+        store(lA, 0);
+        __syncthreads();   // halos of t1 visible
+        t += per;
       }
     }
 
