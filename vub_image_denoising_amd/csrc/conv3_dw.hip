@@ -140,6 +140,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     }
     for (int c = tid; c < CK; c += NT) alds[c] = d.gate_alpha[c];
   }
+  __syncthreads();   // the gate slopes are read by the first halo store (before the prologue barrier)
 
   auto origin = [&](int tt, int& oy, int& ox, int& on) {
     const int tx = tt % tiles_x;

@@ -195,6 +195,8 @@ PLANAR = os.environ.get("RDN_PLANAR", "1") != "0"
 # gated level-0 convs: input + weight gradient in one fused kernel on the compute
 # stream (rdn_conv_dgrad_wgrad) instead of dgrad there and wgrad on the side stream
 FUSE_DW = os.environ.get("RDN_DW", "1") != "0"
+# where the fused layers' split-K reduce runs: "side" (beside the dgrad chain) or "main"
+DW_REDUCE = os.environ.get("RDN_DW_REDUCE", "side")
 # extra elements between two planes (keeps plane starts off power-of-two strides)
 PLANE_PAD = int(os.environ.get("RDN_PLANE_PAD", "0"))
 
@@ -962,7 +964,10 @@ class UNetEngine:
                         tr.stop(tok)
                     if rc:
                         H.check(rc, f"dgrad[{L.name}]")
-            if side is not None:
+            rst = sst   # stream of this layer's reduce
+            if dw and DW_REDUCE == "main":
+                rst = st
+            elif side is not None:
                 side.wait_event(L.extra["ev_ready"])
             if not dw:
                 tok = tr.start(info["wgrad"], side) if tr is not None else None
@@ -975,11 +980,11 @@ class UNetEngine:
             part_splits = 0 if fused else lib.rdn_prelu_bwd_blocks(self.code, P, L.cout_pad)
             ow, ob, oa = L.extra["goff"]
             rc = lib.rdn_wgrad_reduce(L.wgrad_desc.ws, splits, mdim, ndim, ndim_real, taps, gbase + ow, 1, pws,
-                                      part_splits, gbase + oa, gbase + ob, sst)
+                                      part_splits, gbase + oa, gbase + ob, rst)
             if rc:
                 H.check(rc, f"wgrad_reduce[{L.name}]")
             if side is not None:
-                L.extra["ev_done"].record(side)
+                L.extra["ev_done"].record(main if rst == st else side)
             if sync is not None:
                 sync.params_done(L.extra["pidx"], stream=side)
         if side is not None:
