@@ -1,0 +1,178 @@
+"""Every BASELINE config checked at its OWN shape (BASELINE.json `configs`).
+
+* config 4 — ``diffusion_RDUnet_direct.py:198-201`` direct_sampling (one UNet call
+  at t = 1) on a batch of 64 x 3 x 512 x 512, hipGraph-captured (SamplerGraph),
+  bf16: images 0 and 63 against the fp32 CPU oracle's forward of those two images
+  (images never interact in the network, so two CPU forwards check the batched
+  launch, whose grids, BN choices and persistent-tile plans are the 512^2 ones);
+  and fp32 at batch 2 x 512^2 against the oracle at the north_star's 1e-3.
+* config 3 — the data-parallel step as bench.py runs it on the 8-GPU node: an RCCL
+  ("nccl") process group, ddp.GradSync attached, the whole step captured by
+  train_graph.TrainStepGraph (RCCL all_reduce + work.wait() inside the hipGraph).
+  On the one GPU of the test box the group has world size 1, so the all-reduce is
+  the identity and every replay must equal, bit for bit, the same steps taken
+  eagerly with GradSync and the same graph without GradSync.
+
+bf16 budget for the forward (test_gpu_fullsize.py's derivation, forward half):
+bf16 unit roundoff 2^-9 ~ 2e-3 per rounding, ~35 layers each rounding its
+activations once: sqrt(35) * 2e-3 ~ 1.2e-2 relative on the network's correction
+``y - x`` (the denoised image minus its input, which the global residual adds
+back exactly in fp32); bound 3e-2 (2.5x margin); on y itself (values ~1) 5e-3.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from oracle import rdunet_ref as R  # noqa: E402
+from oracle.weights import make_params  # noqa: E402
+
+
+def _params(seed=9):
+    return {k: torch.from_numpy(v) for k, v in make_params(R.param_shapes(32), seed).items()}
+
+
+def _dm(dtype):
+    import vub_image_denoising_amd as vm
+    from vub_image_denoising_amd.diffusion_RDUnet_direct import DiffusionModel
+    dm = DiffusionModel(vm.RDUNet_T(base_filters=32), timesteps=20)
+    dm.unet.load_state_dict(_params())
+    dm = dm.cuda().eval()
+    dm.unet.set_compute_dtype(dtype)
+    return dm
+
+
+def _oracle_direct(x):
+    torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count())
+    p = _params()
+    with torch.no_grad():   # image by image: one 512^2 fp32 forward at a time
+        return torch.cat([R.direct_sampling(lambda xx, tt: R.rdunet_t_forward(p, xx, tt), x[i:i + 1])
+                          for i in range(x.size(0))])
+
+
+def _rel(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).norm() / b.norm()).item()
+
+
+def test_direct_sampling_512_b64_bf16_graph():
+    from vub_image_denoising_amd.sampling import SamplerGraph
+    B, S = 64, 512
+    g = torch.Generator().manual_seed(404)
+    # two probe images generated on the host; the other 62 on the device
+    probe = (torch.rand(2, 3, S, S, generator=g) * 2 - 1).clamp(-1, 1)
+    probe = (probe + (25 / 255 * 2) * torch.randn(2, 3, S, S, generator=g))
+    x = torch.rand(B, 3, S, S, device="cuda", generator=torch.Generator(device="cuda").manual_seed(3)) * 2 - 1
+    x[0].copy_(probe[0])
+    x[B - 1].copy_(probe[1])
+    dm = _dm("bf16")
+    sg = SamplerGraph(dm, tuple(x.shape), direct=True)
+    y = sg(x)
+    torch.cuda.synchronize()
+    assert torch.isfinite(y).all()
+    y2 = sg(x).clone()               # a replay of the captured graph is deterministic
+    assert torch.equal(y, y2)
+    got = y[[0, B - 1]].cpu()
+    ref = _oracle_direct(probe)
+    r_y = _rel(got, ref)
+    r_c = _rel(got - probe, ref - probe)
+    print(f"direct_sampling 64x512^2 bf16: images 0/63 rel err y {r_y:.2e}, correction y-x {r_c:.2e}")
+    assert r_y <= 5e-3 and r_c <= 3e-2
+    # the replay path equals the eager direct_sampling call of the same batch
+    with torch.no_grad():
+        ye = dm.direct_sampling(x)
+    assert torch.equal(ye[[0, B - 1]].cpu(), got)
+
+
+def test_direct_sampling_512_b2_fp32():
+    from vub_image_denoising_amd.sampling import SamplerGraph
+    g = torch.Generator().manual_seed(405)
+    x = torch.rand(2, 3, 512, 512, generator=g) * 2 - 1
+    x = x + (50 / 255 * 2) * torch.randn(2, 3, 512, 512, generator=g)
+    dm = _dm("fp32")
+    y = SamplerGraph(dm, tuple(x.shape), direct=True)(x.cuda()).cpu()
+    ref = _oracle_direct(x)
+    r_y, r_c = _rel(y, ref), _rel(y - x, ref - x)
+    print(f"direct_sampling 2x512^2 fp32: rel err y {r_y:.2e}, correction {r_c:.2e}")
+    assert r_y <= 1e-3 and r_c <= 1e-3
+
+
+# ----------------------------------------------------------------- config 3
+def _rccl_worker(init_file, q):
+    """World-size-1 RCCL group: GradSync + TrainStepGraph vs eager vs no-sync graph."""
+    try:
+        import torch.distributed as dist
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        dist.init_process_group("nccl", init_method=f"file://{init_file}", rank=0, world_size=1, device_id=dev)
+        import vub_image_denoising_amd as vm
+        from vub_image_denoising_amd.ddp import GradSync
+        from vub_image_denoising_amd.diffusion_RDUnet import DiffusionModel, train_step_device
+        from vub_image_denoising_amd.optim import FusedAdamW
+        from vub_image_denoising_amd.train_graph import TrainStepGraph
+        shape = (4, 3, 64, 64)
+
+        def make(sync):
+            torch.manual_seed(0)
+            m = DiffusionModel(vm.RDUNet_T(base_filters=32), timesteps=20).cuda()
+            m.unet.set_compute_dtype("bf16")
+            # build the flat buffer (and the engine) with a throw-away step
+            gz = torch.zeros(shape, device=dev)
+            o0 = torch.optim.SGD(m.parameters(), lr=0.0)
+            train_step_device(m, gz, gz, o0, 'uniform', 1.0, t=torch.zeros(4, device=dev))
+            o = FusedAdamW(m.parameters(), lr=1e-3, weight_decay=1e-2)
+            if sync:   # small buckets: several all-reduces per backward, bucket edges at fused layers
+                m.unet._rdn_flat.grad_sync = GradSync(m.unet._rdn_flat, bucket_mb=0.05)
+            return m, o
+
+        g = torch.Generator().manual_seed(12)
+        data = []
+        for _ in range(4):
+            c = torch.rand(shape, generator=g) * 2 - 1
+            n = c + 0.2 * torch.randn(shape, generator=g)
+            t = torch.randint(0, 21, (shape[0],), generator=g).float()
+            data.append((c.to(dev), n.to(dev), t.to(dev)))
+        mE, oE = make(True)     # eager, RCCL
+        mG, oG = make(True)     # graph, RCCL inside the capture
+        mN, oN = make(False)    # graph, no GradSync
+        gG = TrainStepGraph(mG, oG, shape, t_input=True)
+        gN = TrainStepGraph(mN, oN, shape, t_input=True)
+        nb = len(mG.unet._rdn_flat.grad_sync.buckets)
+        for c, n, t in data:
+            le = train_step_device(mE, c, n, oE, 'uniform', 1.0, t=t)
+            oE.step()
+            lg = gG(c, n, t).clone()
+            ln = gN(c, n, t).clone()
+            if not (torch.equal(le, lg) and torch.equal(lg, ln)):
+                raise AssertionError(f"losses differ: eager {le.item()} graph {lg.item()} nosync {ln.item()}")
+        torch.cuda.synchronize()
+        fE, fG, fN = (m.unet._rdn_flat.flat for m in (mE, mG, mN))
+        res = (bool(torch.equal(fE, fG)), bool(torch.equal(fG, fN)), nb, gG.graph_nodes)
+        dist.destroy_process_group()
+        q.put(res)
+    except Exception as e:  # report instead of hanging the parent on q.get
+        import traceback
+        q.put(repr(e) + "\n" + traceback.format_exc())
+
+
+def test_rccl_world1_graph_captured_gradsync(tmp_path):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(str(tmp_path / "rdv"), q))
+    p.start()
+    try:
+        res = q.get(timeout=110)
+    finally:
+        p.join(timeout=30)
+        if p.is_alive():
+            p.kill()
+    assert not isinstance(res, str), res
+    same_eager, same_nosync, nb, nodes = res
+    print(f"RCCL world 1: {nb} buckets, graph nodes {nodes}; replay == eager: {same_eager}, == no-sync: {same_nosync}")
+    assert nb > 1
+    assert same_eager and same_nosync
+    assert p.exitcode == 0

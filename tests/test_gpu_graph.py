@@ -88,6 +88,30 @@ def test_graph_rng_draws_match_eager():
     _same_state(mA, oA, mB, oB)
 
 
+def test_graph_resume_after_capture():
+    """load_state_dict on a bound optimizer whose step a graph has captured (the
+    resume-after-construction path): the replays continue from the LOADED moments
+    and step count, exactly as an eager optimizer resumed from the same state."""
+    import io
+    from vub_image_denoising_amd.train_graph import TrainStepGraph
+    data = _batches(4)
+    mA, mB = _model(), _model()
+    oA, oB = _opt(mA), _opt(mB)
+    g = TrainStepGraph(mB, oB, SHAPE, t_input=True)
+    for clean, noisy, t in data[:2]:       # a checkpoint after two steps
+        _eager(mA, oA, clean, noisy, t)
+    buf = io.BytesIO()
+    torch.save({"m": mA.state_dict(), "o": oA.state_dict()}, buf)
+    g(*data[3])                              # the graph's model drifts elsewhere first
+    buf.seek(0)
+    ck = torch.load(buf, map_location="cuda", weights_only=True)
+    mB.load_state_dict(ck["m"])
+    oB.load_state_dict(ck["o"])
+    for clean, noisy, t in data[2:]:
+        assert torch.equal(_eager(mA, oA, clean, noisy, t), g(clean, noisy, t))
+    _same_state(mA, oA, mB, oB)
+
+
 def _median_ms(fn, n=11):
     ts = []
     for _ in range(n):

@@ -110,6 +110,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
   unsigned char* const dyh = lds + Cfg::W_BYTES;
   unsigned char* const xh = dyh + Cfg::D_BYTES;
   float* const alds = (float*)(xh + Cfg::XB * Cfg::X_BYTES + Cfg::CT_BYTES);
+  float* const red = (float*)(lds + Cfg::W_BYTES);   // partial reduction (aliases the halos after the loops)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const bool dwave = wave < 4;                          // role (wave-uniform)
@@ -330,26 +331,13 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     if (t < t_hi)
       while (step(lA, gA, lB, gB, eC, eN) && step(lB, gB, lA, gA, eN, eC)) {}
 
-    // dalpha / dbias partials of this split, fixed order
+    // dalpha / dbias partials of this split into LDS (the loop ended with a barrier
+    // that both roles passed, so the halo area is free); summed below
     if (wg.part) {
-      float* red = (float*)(lds + Cfg::W_BYTES);   // the loop ended with a barrier
 #pragma unroll
       for (int k = 0; k < VEC; ++k) {
         red[rt * VEC + k] = sa[k];
         red[NR * VEC + rt * VEC + k] = sb[k];
-      }
-      __syncthreads();   // D waves only (W waves never pass a barrier after their loop)
-      if (rt < CK) {
-        const int cg = rt / VEC, k = rt % VEC;
-        float a = 0.f, b = 0.f;
-        for (int rr = 0; rr < NR / DU; ++rr) {
-          a += red[(rr * DU + cg) * VEC + k];
-          b += red[NR * VEC + (rr * DU + cg) * VEC + k];
-        }
-        if (rt < wg.mdim) {
-          wg.part[((int64_t)blockIdx.x * 2 + 0) * wg.mdim + rt] = a;
-          wg.part[((int64_t)blockIdx.x * 2 + 1) * wg.mdim + rt] = b;
-        }
       }
     }
   } else {
@@ -499,6 +487,26 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
           const int m = i * 16 + g * 4 + e;
           if (m < wg.mdim) ws[(int64_t)m * ncol_all + col] = accW[i][j][e];
         }
+    }
+  }
+
+  // dalpha / dbias partials of this split, fixed order.  Both roles arrive at this
+  // ONE barrier (each role's loop passes the same number of barriers per tile), so
+  // no barrier is ever role-divergent.
+  if (wg.part) {
+    __syncthreads();
+    if (dwave && rt < CK) {
+      constexpr int DUC = CK / VEC;
+      const int cg = rt / VEC, k = rt % VEC;
+      float a = 0.f, b = 0.f;
+      for (int rr = 0; rr < NR / DUC; ++rr) {
+        a += red[(rr * DUC + cg) * VEC + k];
+        b += red[NR * VEC + (rr * DUC + cg) * VEC + k];
+      }
+      if (rt < wg.mdim) {
+        wg.part[((int64_t)blockIdx.x * 2 + 0) * wg.mdim + rt] = a;
+        wg.part[((int64_t)blockIdx.x * 2 + 1) * wg.mdim + rt] = b;
+      }
     }
   }
 }

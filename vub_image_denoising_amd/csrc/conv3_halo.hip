@@ -463,6 +463,8 @@ int rdn_conv3_launch(const rdn_conv_desc* d, hipStream_t st) {
     return RDN_E_SHAPE;
   }
   if (d->dtype == RDN_BF16) {
+    const int big = rdn_conv3_big_launch(d, ck, st);   // MFMA-heavy level-1..3 shapes (conv3_big.hip)
+    if (big <= 0) return big;
     const int wsd = rdn_conv3_wsd_launch(d, ck, st);   // full-tile level-0/1 shapes (conv3_wsd.hip)
     if (wsd <= 0) return wsd;
     const int ws = rdn_conv3_ws_launch(d, ck, st);

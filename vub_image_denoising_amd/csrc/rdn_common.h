@@ -138,6 +138,7 @@ int rdn_conv3_chunk_impl(int cin, int dtype);
 int rdn_conv3_chunk_pow2(int cin, int cap);
 int rdn_conv3_ws_launch(const rdn_conv_desc* d, int ck, hipStream_t st);
 int rdn_conv3_wsd_launch(const rdn_conv_desc* d, int ck, hipStream_t st);
+int rdn_conv3_big_launch(const rdn_conv_desc* d, int ck, hipStream_t st);
 int rdn_wgrad3_launch(const rdn_wgrad_desc* d, hipStream_t st);
 int rdn_wgrad3_splits(const rdn_wgrad_desc* d);
 int rdn_wgrad3_chunks(const rdn_wgrad_desc* d);

@@ -76,6 +76,7 @@ class GradSync:
         self._works = []
         self._remaining = list(self.counts)
         self._launched = [False] * len(self.buckets)
+        self._srcs = [[] for _ in self.buckets]
         self._inv = None
         self.buf = fp.gflat
 
@@ -87,26 +88,38 @@ class GradSync:
         self._works = []
         self._remaining = list(self.counts)
         self._launched = [False] * len(self.buckets)
+        self._srcs = [[] for _ in self.buckets]
 
     def params_done(self, indices, stream=None):
         """The gradients of these parameter indices are final on ``stream`` (the
-        engine's weight-gradient stream; default: the current stream); launch
-        every bucket that just became complete.  Every rank runs the same
+        stream whose launch wrote them last -- the engine's weight-gradient side
+        stream, or the compute stream for the fused layers; default: the current
+        stream); launch every bucket that just became complete, ordered after
+        EVERY stream that wrote one of its gradients.  Every rank runs the same
         backward, so buckets are issued in the same order everywhere."""
+        if self.overlap:
+            s = stream if stream is not None else torch.cuda.current_stream()
         for i in indices:
             b = self.param_bucket[i]
+            if self.overlap and all(x.cuda_stream != s.cuda_stream for x in self._srcs[b]):
+                self._srcs[b].append(s)
             self._remaining[b] -= 1
             if self._remaining[b] == 0:
-                self._launch(b, stream)
+                self._launch(b)
 
-    def _launch(self, b, src=None):
+    def _launch(self, b):
         if self._launched[b]:
             return
         self._launched[b] = True
         lo, hi = self.buckets[b]
         view = self.buf[lo:hi]
         if self.overlap:
-            self.stream.wait_stream(src if src is not None else torch.cuda.current_stream())
+            # the host issues this after every launch that wrote the bucket, so
+            # waiting on each writer stream's current tail orders the all-reduce
+            # after all of them (and the finish() path after the compute stream)
+            srcs = self._srcs[b] or [torch.cuda.current_stream()]
+            for s in srcs:
+                self.stream.wait_stream(s)
             with torch.cuda.stream(self.stream):
                 self._works.append(dist.all_reduce(view, group=self.group, async_op=True))
         else:
@@ -115,6 +128,8 @@ class GradSync:
     def finish(self):
         """Launch what is left (in bucket order), wait, and average."""
         for b in range(len(self.buckets)):
+            if not self._launched[b] and self.overlap:
+                self._srcs[b].append(torch.cuda.current_stream())
             self._launch(b)
         for w in self._works:
             w.wait()

@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import warnings
 import weakref
 from dataclasses import dataclass, field
 
@@ -586,6 +587,7 @@ class UNetEngine:
             self._build_bwd()
         self._build_info()
         self.lease = None   # weakref to the autograd graph's lease while it owns the activations
+        self.lease_seq = 0
 
     # ------------------------------------------------------------------
     def _out_level(self, L):
@@ -987,8 +989,8 @@ class UNetEngine:
                 H.check(rc, f"wgrad_reduce[{L.name}]")
             if side is not None:
                 L.extra["ev_done"].record(main if rst == st else side)
-            if sync is not None:
-                sync.params_done(L.extra["pidx"], stream=side)
+            if sync is not None:   # the stream this layer's gradients were completed on
+                sync.params_done(L.extra["pidx"], stream=None if side is None else (main if rst == st else side))
         if side is not None:
             self.ev_end.record(side)
             main.wait_event(self.ev_end)
@@ -1018,6 +1020,12 @@ class _Lease:
 
 def _engine_free(eng) -> bool:
     return eng.lease is None or eng.lease() is None
+
+
+# full-activation engines per (shape, dtype) that grad-enabled forwards may hold at once
+MAX_TRAIN_ENGINES = 4
+_LEASE_SEQ = [0]
+_WARNED_POOL: list = []
 
 
 class _EngineFunction(torch.autograd.Function):
@@ -1055,13 +1063,25 @@ def _run(module, key_shape, xs, t, params, make_engine):
         with torch.no_grad():
             return pool[0].forward(xs, t)
     # a graph owns its engine's activations until its backward (or until it is
-    # freed): a second forward before that backward gets a second engine
+    # freed): a second forward before that backward gets a second engine, up to
+    # MAX_TRAIN_ENGINES per shape; past that the least recently leased engine is
+    # taken over and the graph that held it raises if it is ever backwarded
     eng = next((e for e in pool if _engine_free(e)), None)
     if eng is None:
-        eng = make_engine(True)
-        pool.append(eng)
+        if len(pool) < MAX_TRAIN_ENGINES:
+            eng = make_engine(True)
+            pool.append(eng)
+        else:
+            eng = min(pool, key=lambda e: e.lease_seq)
+            if not _WARNED_POOL:
+                _WARNED_POOL.append(True)
+                warnings.warn(f"{type(module).__name__}: {MAX_TRAIN_ENGINES} grad-enabled forwards of one shape are "
+                              "alive without a backward; reusing the oldest one's saved activations (its backward "
+                              "will raise). Run evaluation under torch.no_grad().", RuntimeWarning, stacklevel=3)
     lease = _Lease()
     eng.lease = weakref.ref(lease)
+    _LEASE_SEQ[0] += 1
+    eng.lease_seq = _LEASE_SEQ[0]
     return _EngineFunction.apply(eng, lease, t, len(xs), *xs, *params.params)
 
 

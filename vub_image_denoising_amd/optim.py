@@ -39,30 +39,40 @@ class FusedAdam(torch.optim.Optimizer):
         if self._fp is not fp:
             # moments already in self.state (a load_state_dict before the first step,
             # or a previous flat buffer) are carried over into the new flat buffers
-            old = {p: self.state[p] for p in fp.params if p in self.state}
             self._fp = fp
             self._m = torch.zeros_like(fp.flat)
             self._v = torch.zeros_like(fp.flat)
             self._steps = torch.zeros((), dtype=torch.float32)
-            steps = set()
-            for p, off in zip(fp.params, fp.offsets):
-                n = p.numel()
-                st = old.get(p)
-                if st and "exp_avg" in st:
-                    self._m[off:off + n].copy_(st["exp_avg"].reshape(-1))
-                    self._v[off:off + n].copy_(st["exp_avg_sq"].reshape(-1))
-                    steps.add(int(float(st["step"])))
-            if len(steps) > 1:
-                raise RuntimeError(f"FusedAdam: parameters were saved at different step counts {sorted(steps)}")
-            self._step = steps.pop() if steps else 0
-            self._steps.fill_(self._step)
-            if self._step_dev is not None:
-                if self._step_dev.device == fp.device:
-                    self._step_dev.fill_(self._step)
-                else:
-                    self._step_dev = torch.full((), self._step, dtype=torch.int64, device=fp.device)
-            self._views()
+            self._load_moments()
         return fp
+
+    def _load_moments(self):
+        """Copy the moments / step count held in ``self.state`` (torch's per-parameter
+        format) INTO the existing flat buffers and device step counter, then make the
+        state entries views of them again.  In place, so a TrainStepGraph captured
+        over these buffers keeps replaying on the loaded state."""
+        fp = self._fp
+        old = {p: self.state[p] for p in fp.params if p in self.state}
+        steps = set()
+        self._m.zero_()
+        self._v.zero_()
+        for p, off in zip(fp.params, fp.offsets):
+            n = p.numel()
+            st = old.get(p)
+            if st and "exp_avg" in st:
+                self._m[off:off + n].copy_(st["exp_avg"].reshape(-1))
+                self._v[off:off + n].copy_(st["exp_avg_sq"].reshape(-1))
+                steps.add(int(float(st["step"])))
+        if len(steps) > 1:
+            raise RuntimeError(f"FusedAdam: parameters were saved at different step counts {sorted(steps)}")
+        self._step = steps.pop() if steps else 0
+        self._steps.fill_(self._step)
+        if self._step_dev is not None:
+            if self._step_dev.device == fp.device:
+                self._step_dev.fill_(self._step)
+            else:
+                self._step_dev = torch.full((), self._step, dtype=torch.int64, device=fp.device)
+        self._views()
 
     def use_device_step(self):
         """Keep the step count in device memory, incremented and read by the
@@ -88,7 +98,14 @@ class FusedAdam(torch.optim.Optimizer):
 
     def load_state_dict(self, state_dict):
         super().load_state_dict(state_dict)
-        if self._fp is not None:          # already bound: rebind, copying the loaded state in
+        if self._fp is None:
+            return                        # moments are taken over at the first bind
+        fp = find_flat(self.param_groups[0]["params"])
+        if fp is self._fp or fp is None:
+            # same flat buffers (the usual resume): loaded into the existing moment
+            # buffers and step counter, whose addresses a captured graph holds
+            self._load_moments()
+        else:
             self._fp = None
             self._bind()
 

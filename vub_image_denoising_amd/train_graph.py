@@ -65,9 +65,17 @@ class TrainStepGraph:
 
     # ------------------------------------------------------------------
     def _hyper(self):
+        """Everything baked into the captured graph: hyperparameters, the compute
+        dtype, and the addresses of the buffers the optimizer updates (a rebound
+        optimizer or a re-flattened model re-captures instead of replaying onto
+        freed memory)."""
         g = self.opt.param_groups[0]
+        o = self.opt
+        ptrs = tuple(0 if b is None else b.data_ptr()
+                     for b in (getattr(o, "_m", None), getattr(o, "_v", None), o._step_dev,
+                               None if o._fp is None else o._fp.flat))
         return (float(g["lr"]), tuple(g["betas"]), float(g["eps"]), float(g["weight_decay"]), float(self.clip),
-                float(self.opt.grad_scale), self.model.unet.compute_dtype)
+                float(self.opt.grad_scale), self.model.unet.compute_dtype, ptrs)
 
     def _body(self):
         loss = train_step_device(self.model, self.clean, self.noisy, self.opt, self.dist, self.clip, t=self.t)
