@@ -97,7 +97,7 @@ def extra_configs(dev, args):
     conv path's HBM roofline from a serialised profiling pass) and at the
     reference's own precision (fp32, batch 16).  Rank 0 of a 1-GPU run only."""
     out = {}
-    for key, batch, dtype, warm, steps in (("b32", 32, "bf16", 3, args.steps), ("fp32", 16, "fp32", 2, 6)):
+    for key, batch, dtype, warm, steps in (("b32", 32, "bf16", 3, args.steps), ("fp32", 16, "fp32", 2, max(20, args.steps))):
         _log(f"extra config {key}: batch {batch} {dtype}")
         tr = Trainer(dev, batch, args.size, args.base_filters, dtype, graph=args.graph == "on")
         for i in range(warm):
@@ -115,9 +115,11 @@ def extra_configs(dev, args):
     return out
 
 
-def cpu_baseline(seconds=12.0, batch=16, size=256):
+def cpu_baseline(seconds=12.0, batch=16, size=256, steps=3):
     """The CPU oracle's train step (fp32, torch aten on the host cores), at the
-    headline's per-GPU batch: one warm-up step, then whole steps until `seconds`."""
+    headline's per-GPU batch: one batch-2 warm-up step, then `steps` whole batch
+    steps (at least 3), the MEDIAN step time reported (`seconds` is kept for the
+    command line; a B16 step takes ~12 s on 16 host cores)."""
     from oracle import rdunet_ref as R
     from oracle.weights import make_params
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
@@ -127,18 +129,57 @@ def cpu_baseline(seconds=12.0, batch=16, size=256):
     clean = torch.rand(batch, 3, size, size, generator=g) * 2 - 1
     noisy = clean + (25 / 255 * 2) * torch.randn(batch, 3, size, size, generator=g)
     t = torch.randint(0, 21, (batch,), generator=g)
-    R.train_step(params, clean, noisy, t, 20)  # warm-up
-    n, t0 = 0, time.perf_counter()
-    while True:
+    R.train_step(params, clean[:2], noisy[:2], t[:2], 20)  # warm-up (allocator, threads)
+    ts = []
+    for _ in range(max(3, steps)):
+        t0 = time.perf_counter()
         R.train_step(params, clean, noisy, t, 20)
-        n += 1
-        el = time.perf_counter() - t0
-        if el >= seconds or n >= 50:
-            break
-    return {"value": round(batch * n / el, 4), "unit": "images/s", "cores": torch.get_num_threads(),
-            "kind": "port",
-            "sample": f"{n} oracle train steps (fwd+Charbonnier+bwd+clip) of RDUNet_T(32) fp32 at batch {batch} "
-                      f"x 3x{size}x{size}, {el:.1f}s on the host CPU"}
+        ts.append(time.perf_counter() - t0)
+    med = sorted(ts)[len(ts) // 2]
+    return {"value": round(batch / med, 4), "unit": "images/s", "cores": torch.get_num_threads(),
+            "kind": "port", "step_s_median": round(med, 3), "step_s_all": [round(x, 3) for x in ts],
+            "sample": f"median of {len(ts)} oracle train steps (fwd+Charbonnier+bwd+clip) of RDUNet_T(32) fp32 at "
+                      f"batch {batch} x 3x{size}x{size} on the host CPU ({sum(ts):.1f}s timed)"}
+
+
+def config1_forward(dev, reps=5):
+    """BASELINE config 1: RDUNet (UNet/RDUNet_model.py:117-186, base_filters 64)
+    forward on one 1x3x64x64 Gaussian-noise tensor.  The reference runs it on the
+    CPU (the oracle restates that path, timed here on the host cores: median of
+    `reps`); the same call through this build on the GPU (fp32, parity mode) is
+    timed beside it and compared (rel-L2)."""
+    from oracle import rdunet_ref as R
+    from oracle.weights import make_params
+    import vub_image_denoising_amd as vm
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
+    torch.set_num_threads(threads)
+    params = {k: torch.from_numpy(v) for k, v in make_params(R.param_shapes(64, 3, 3), 2).items()}
+    x = torch.randn(1, 3, 64, 64, generator=torch.Generator().manual_seed(1))
+    with torch.no_grad():
+        R.rdunet_forward(params, x)
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            y_cpu = R.rdunet_forward(params, x)
+            ts.append(time.perf_counter() - t0)
+    m = vm.RDUNet(channels=3, base_filters=64)
+    m.load_state_dict(params)
+    m = m.to(dev).eval()
+    xg = x.to(dev)
+    with torch.no_grad():
+        m(xg)
+        torch.cuda.synchronize()
+        tg = []
+        for _ in range(20):
+            t0 = time.perf_counter()
+            y = m(xg)
+            torch.cuda.synchronize()
+            tg.append(time.perf_counter() - t0)
+    rel = ((y.cpu().double() - y_cpu.double()).norm() / y_cpu.double().norm()).item()
+    return {"workload": "RDUNet(channels=3, base_filters=64) forward, 1x3x64x64 Gaussian noise",
+            "cpu_ms_median": round(1e3 * sorted(ts)[reps // 2], 3), "cpu_cores": torch.get_num_threads(),
+            "gpu_fp32_ms_median": round(1e3 * sorted(tg)[10], 3), "gpu_vs_cpu_rel_l2": float(f"{rel:.3e}"),
+            "note": "GPU time is host wall per eager call (launch-bound at this size)"}
 
 
 def _log(msg):
@@ -534,6 +575,8 @@ def main():
         if not (args.no_inference or args.pmc_child) and world == 1:
             _log("sampler measurements")
             infer = inference_bench(dev, args.base_filters)
+            _log("config 1 forward (CPU oracle and GPU)")
+            infer["config1_rdunet64_forward"] = config1_forward(dev)
         out = {
             "metric": "images/sec (256x256x3) RDUNet diffusion train step",
             "value": round(images / el, 2),

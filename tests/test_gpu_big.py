@@ -7,7 +7,7 @@ tile override, desc.bn, bypasses conv3_big).  Both run the same MFMA over the sa
 k sequence on the same bf16 operands, so the outputs must be bit-identical; both
 are also held to torch fp32 math on the CPU at the bf16 budget of
 test_gpu_kernels.py (2e-2).  Shapes are the network's (Unet_model.py:72-89 dense
-convs, :35-43 up convs, their gated input gradients), at batch sizes that clear
+convs, :35-43 up convs, their input gradients), at batch sizes that clear
 the kernel's grid rule, including channel-blocked ("planar") operands, the
 residual / accumulate epilogues and partial edge tiles.
 """
@@ -66,14 +66,17 @@ class Operand:
 
 CASES = [
     # name, N, H, W, cin (K side), x channels, x c0, x planes, ncols, out channels, out c0, out planes,
-    # resid (res channels, c0, climit), gate, accum
-    ("L2_conv3_fwd_resid", 2, 64, 64, 320, 320, 0, 64, 128, 128, 0, 0, (320, 0, 128), False, False),
-    ("L3_conv3_dgrad_gate_accum", 8, 32, 32, 256, 256, 0, 0, 640, 640, 0, 128, None, True, True),
-    ("L1_conv3_fwd_planar_ck32", 1, 128, 128, 160, 160, 0, 32, 64, 64, 0, 0, (160, 0, 64), False, False),
-    ("L1_conv3_dgrad_bn160_gate", 1, 128, 128, 64, 64, 0, 0, 160, 160, 0, 32, None, True, False),
-    ("L2_up_conv_fwd_slice", 2, 64, 64, 384, 384, 0, 0, 128, 320, 0, 64, None, False, False),
-    ("L2_dgrad_bn96_ragged", 4, 40, 56, 64, 64, 0, 0, 192, 192, 0, 0, None, False, True),
+    # resid (res channels, c0, climit), gate, accum -- shapes the dispatch rule gives to conv3_big
+    ("L2_conv3_fwd_resid", 16, 64, 64, 320, 320, 0, 64, 128, 128, 0, 0, (320, 0, 128), False, False),
+    ("L3_conv2_dgrad_accum", 16, 32, 32, 128, 128, 0, 0, 512, 512, 0, 128, None, False, True),
+    ("L2_up2_dgrad_planar_out", 16, 64, 64, 128, 128, 0, 0, 384, 384, 0, 128, None, False, False),
+    ("L2_up_conv_fwd_slice", 16, 64, 64, 384, 384, 0, 0, 128, 320, 0, 64, None, False, False),
+    ("L1_up1_dgrad_bn64", 16, 128, 128, 64, 64, 0, 0, 192, 192, 0, 32, None, False, True),
+    ("L2_ragged_fwd_resid", 25, 72, 56, 256, 256, 0, 64, 128, 128, 0, 0, (256, 0, 128), False, False),
+    ("L3_conv3_fwd_planar_in", 32, 32, 32, 640, 640, 0, 128, 256, 256, 0, 0, (640, 0, 256), False, False),
 ]
+# gated input gradients are not taken by conv3_big (they stay on conv3_halo)
+GATED = ("L3_gated_dgrad", 8, 32, 32, 256, 256, 0, 0, 640, 640, 0, 128, None, True, True)
 
 
 @pytest.fixture(autouse=True)
@@ -87,7 +90,8 @@ def _run(case, force_halo, ops):
     x, wp, b, a, out0, pre, res, gt, ga = ops
     out = Operand(N * Hh * Ww, oc, ocb, fill=False)
     out.t.copy_(out0.t)
-    flags = 0 if gate else (H.EPI_BIAS | H.EPI_PRELU | H.EPI_STORE_PRE)
+    fwd = _is_fwd(case)
+    flags = (H.EPI_BIAS | H.EPI_PRELU | H.EPI_STORE_PRE) if fwd else 0
     if resid:
         flags |= H.EPI_RESID
     if accum:
@@ -96,7 +100,7 @@ def _run(case, force_halo, ops):
                    x=x.t.data_ptr(), x_ps=x.ps, x_c0=xc0, x_pl=x.pl, wp=wp.data_ptr(), kp=wp.shape[1], ncols=ncols,
                    cout=ncols, bias=b.data_ptr(), alpha=a.data_ptr(), out=out.t.data_ptr(), out_ps=out.ps,
                    out_c0=oc0, out_pl=out.pl)
-    if not gate:
+    if fwd:
         d.pre, d.pre_ps = pre.data_ptr(), ncols
     if resid:
         d.res, d.res_ps, d.res_c0, d.res_pl, d.res_climit = res.t.data_ptr(), res.ps, resid[1], res.pl, resid[2]
@@ -111,7 +115,11 @@ def _run(case, force_halo, ops):
     return out, buf.value.decode()
 
 
-@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def _is_fwd(case):
+    return "_fwd" in case[0] and not case[13]
+
+
+@pytest.mark.parametrize("case", CASES + [GATED], ids=[c[0] for c in CASES + [GATED]])
 def test_conv3_big_vs_halo_and_torch(case):
     (name, N, Hh, Ww, cin, xc, xc0, xcb, ncols, oc, oc0, ocb, resid, gate, accum) = case
     P = N * Hh * Ww
@@ -130,7 +138,7 @@ def test_conv3_big_vs_halo_and_torch(case):
     pre_big = pre.clone()
     y_halo, k_halo = _run(case, True, ops)
     print(f"{name}: default -> {k_big}; override -> {k_halo}")
-    assert k_big.startswith("conv3_big_kernel"), k_big
+    assert k_big.startswith("conv3_halo_kernel" if gate else "conv3_big_kernel"), k_big
     assert k_halo.startswith("conv3_halo_kernel"), k_halo
     # torch fp32 reference on the bf16 operands
     xs = x.nchw(N, Hh, Ww, xc0, cin)
@@ -138,8 +146,9 @@ def test_conv3_big_vs_halo_and_torch(case):
         g = gt.nchw(N, Hh, Ww, 0, cin)
         xs = torch.where(g > 0, xs, ga.cpu().view(1, -1, 1, 1) * xs).to(BF).float()
     wr = w.cpu().to(BF).float()
-    core = F.conv2d(xs, wr, None if gate else b.cpu(), padding=1)
-    ref = core if gate else F.prelu(core, a.cpu())
+    fwd = _is_fwd(case)
+    core = F.conv2d(xs, wr, b.cpu() if fwd else None, padding=1)
+    ref = F.prelu(core, a.cpu()) if fwd else core
     if resid:
         rr = res.nchw(N, Hh, Ww, resid[1], ncols).clone()
         rr[:, resid[2]:] = 0
@@ -152,7 +161,7 @@ def test_conv3_big_vs_halo_and_torch(case):
     ndiff = (y_big.t != y_halo.t).sum().item()
     print(f"{name}: rel err vs torch {e:.2e}; bit-identical to conv3_halo: {same} ({ndiff} differing)")
     assert e < 2e-2
-    if not gate:
+    if fwd:
         assert _rel(pre_big[:, :ncols].float().cpu().reshape(N, Hh, Ww, ncols).permute(0, 3, 1, 2), core) < 2e-2
     # channels outside [oc0, oc0 + ncols) untouched
     if oc > ncols:

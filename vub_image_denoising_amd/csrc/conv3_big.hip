@@ -1,197 +1,221 @@
-// 3x3 / pad 1 / stride 1 convolution as an implicit GEMM on large tiles (gfx950,
-// bf16 MFMA): the MFMA-heavy convolutions of levels 1-3 in forward
-// (Unet_model.py:72-89 dense convs, :35-43 up convs) and their input gradients (the
-// same conv over dYpre with rotated, transposed weights; PReLU-backward gate
-// optionally fused into the halo loader, as conv3_halo).
+// 3x3 / pad 1 / stride 1 convolution as a persistent implicit GEMM on large tiles
+// (gfx950, bf16 MFMA, LDS-DMA staging): the MFMA-heavy convolutions of levels 1-3
+// in forward (Unet_model.py:72-89 dense convs, :35-43 up convs) and their input
+// gradients (the same conv over dYpre with rotated, transposed weights).
 //
-// Why a second halo kernel: conv3_halo (4 waves, 8 x 16 pixels x <= 128 columns)
-// re-streams the weights from L2 for every 128 pixels and meets a barrier every
-// 16-32 MFMAs per wave; at levels 2/3 it ran at 0.25-0.3 of the MFMA peak with
-// 44 % of its wave cycles parked at waits.  Here:
+// Why: conv3_halo (4 waves, 8 x 16 pixels x <= 128 columns) re-streams the weights
+// from L2 for every 128 pixels and meets a barrier every 16-32 MFMAs per wave; at
+// levels 2/3 it ran at 0.28-0.36 of the MFMA peak.  A first large-tile version of
+// this kernel (one 16 x 16-pixel tile per block, register-staged, r03) showed what
+// else limits: a level-2 grid is ONE round of blocks over the CUs, so every block
+// loads its first halo, multiplies and writes its outputs in lock step with all
+// the others, and the only variant that beat conv3_halo ran two blocks per CU.
+// Here:
 //
-// * block = 512 threads (8 waves, one block per CU) = a TH x 16 pixel tile (TH = 16:
-//   256 pixels) x BN output columns; every weight byte staged in LDS feeds 256
-//   pixels (half the L2 weight stream of the 128-pixel tile) and every wave owns a
-//   64 x 64 (or 32 x 64 / 64 x 32) accumulator tile: 16 MFMAs per 8 fragment reads;
-// * one LDS weight stage = TWO 64-deep K stages (256-B rows padded to 288 B:
-//   conflict-free ds_read_b128), double buffered and register staged one stage
-//   ahead, so a wave runs 32 MFMAs (64 x 64 tile) between two barriers;
-// * the input halo [(TH+2) x 18][CK] of a channel chunk is loaded ONCE for all 9
-//   taps, the next chunk's halo is prefetched into registers during the current
-//   chunk;
-// * MFMA operands are swapped (A = weights, B = pixels): a lane ends with four
-//   consecutive output channels of one pixel, written to the fp32 epilogue tile in
-//   LDS as one 16-byte store; the epilogue then applies bias / PReLU-input store /
-//   PReLU / residual / accumulate as 16-byte NHWC units (conv3_halo's epilogue).
+// * block = 512 threads (8 waves), one per CU, PERSISTENT over work items (a 16 x 16
+//   pixel tile x BN output columns): the next item's first halo and weight stage
+//   are in flight during the current item's last stages, and the epilogue goes
+//   from the accumulators straight to global memory (buffer stores, no LDS tile,
+//   no barrier), so its stores drain while the next item multiplies;
+// * every weight byte staged in LDS feeds 256 pixels; each wave owns a 64 x 64
+//   (64 x 32) accumulator tile: 128 B/clk/CU of LDS fragment reads at the MFMA
+//   rate, half the LDS bandwidth;
+// * everything reaches LDS by LDS-DMA (global_load_lds_dwordx4, no VGPR staging):
+//   the input halo [18 x 18][CK] of a channel chunk (double buffered, loaded ONCE
+//   for all 9 taps, one chunk ahead) and the weights (one LDS stage = two 64-deep
+//   K stages, double buffered, one stage ahead); each wave waits for its own DMAs
+//   with a counted vmcnt and a raw barrier publishes them.  A DMA wave-instruction
+//   writes 1 KB linearly, so the LDS images are dense and bank conflicts of the
+//   ds_read_b128 fragment reads are removed by XOR-swizzling 16-byte units on the
+//   SOURCE side (checked exhaustively for the fragment patterns, every tap shift);
+// * MFMA operands are swapped (A = weights, B = pixels): a lane holds four
+//   consecutive output channels of one pixel -- the 8-byte epilogue unit.
 //
 // Packed weights as for conv3_halo (rdn_pack_weights with ck > 0):
 //   P[n][chunk*KC + tap*CK + ci],  KC = roundup(9*CK, 64).
 #include "conv3_tile.h"
 
 #include <cstdlib>
-#include <utility>
 
 namespace {
 
-template <typename F, int... I>
-__device__ __forceinline__ void static_for_impl(F& f, std::integer_sequence<int, I...>) {
-  (f(std::integral_constant<int, I>{}), ...);
+__device__ __attribute__((aligned(64))) unsigned int g_big_zero[16];
+
+template <int N>
+__device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+// One LDS-DMA wave-instruction: 16 B per lane from `src` to LDS byte dst + lane*16
+// (dst wave-uniform, in M0).  Inline asm, so that the compiler does not treat the
+// LDS as pending on the VM counter (with the builtin it waits vmcnt(0) before every
+// ds_read of the array); the counted waits in the loop are the ordering.
+__device__ __forceinline__ void glds16(const void* src, unsigned dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(__builtin_amdgcn_readfirstlane(dst))
+               : "memory");
 }
-// f(integral_constant<int, 0>) ... f(integral_constant<int, N-1>), unrolled
-template <int N, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  static_for_impl(f, std::make_integer_sequence<int, N>{});
+__device__ __forceinline__ unsigned lds_addr(const unsigned char* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) unsigned char*)p;
 }
 
 constexpr int NTB = 512;
 constexpr int TWB = 16;
+constexpr int RS = TWB + 2;        // halo pixels per halo row
 constexpr int LDS_CAP = 160 * 1024;
+constexpr int COL_MAX = 640;       // bias / PReLU-slope table in LDS
 
-template <int TH, int BN, int WM, int CK, bool GATE>
-struct BigCfg {
+// epilogue modes (compile-time): forward = bias + PReLU-input store + PReLU
+// (+ residual); input gradient = plain (+ accumulate | + residual)
+enum { EP_FWD = 0, EP_FWD_RES = 1, EP_PLAIN = 2, EP_ACC = 3, EP_RES = 4 };
+
+// halo image swizzle: physical 16-B unit of logical unit u at halo column x
+template <int CK>
+__device__ __forceinline__ int hswz(int u, int x) {
+  return CK == 64 ? (u ^ (x & 7)) : (u ^ ((x >> 1) & 3));
+}
+
+template <int TH, int BN, int WM, int CK>
+struct PtCfg {
   static constexpr int BM = TH * TWB;
-  static constexpr int HWP = (TH + 2) * (TWB + 2);            // halo pixels
-  static constexpr int HROW = c3::HaloRow<CK * 2>::V;         // bytes per halo pixel
-  static constexpr int HALO_BYTES = (HWP * HROW + 15) / 16 * 16;
-  static constexpr int KC = (9 * CK + 63) / 64 * 64;          // packed K per chunk
-  static constexpr int SPC = KC / 64;                          // 64-deep K stages per chunk
-  static constexpr int SS = (SPC + 1) / 2;                     // LDS stages (pairs) per chunk
-  static constexpr int RW = 288;                               // LDS weight row: 2 x 128 B + 32 B pad
+  static constexpr int HWP = (TH + 2) * RS;                    // halo pixels
+  static constexpr int RB = CK * 2;                            // bytes per halo pixel
+  static constexpr int H_PIECES = (HWP * RB + 1023) / 1024;    // 1-KB DMA pieces per halo
+  static constexpr int HALO_BYTES = H_PIECES * 1024;
+  static constexpr int KC = (9 * CK + 63) / 64 * 64;           // packed K per chunk
+  static constexpr int SPC = KC / 64;                           // 64-deep K stages per chunk
+  static constexpr int SS = (SPC + 1) / 2;                      // LDS stages (pairs) per chunk
+  static constexpr int RW = 256;                                // LDS weight row: 2 x 128 B
   static constexpr int W_BYTES = BN * RW;
-  static constexpr int MAIN = HALO_BYTES + 2 * W_BYTES;
-  static constexpr int CROW = BN * 4 + 16;                     // epilogue fp32 row (bytes)
-  static constexpr int EPI = BM * CROW;
-  static constexpr int LDS = MAIN > EPI ? MAIN : EPI;
+  static constexpr int W_PIECES = W_BYTES / 1024;
+  static constexpr int W_PW = W_PIECES / 8;                     // weight pieces per wave per stage
+  static constexpr int TAB = 2 * COL_MAX * 4;
+  static constexpr int LDS = 2 * HALO_BYTES + 2 * W_BYTES + TAB;
   static constexpr int WN = 8 / WM;
-  static constexpr int WTM = BM / WM, WTN = BN / WN;           // wave tile (pixels x columns)
+  static constexpr int WTM = BM / WM, WTN = BN / WN;            // wave tile (pixels x columns)
   static constexpr int MT = WTM / 16, NTL = WTN / 16;
-  static constexpr int HU = CK / 8;                            // 16-B units per halo pixel
-  static constexpr int H_UNITS = HWP * HU;
-  static constexpr int H_IT = (H_UNITS + NTB - 1) / NTB;
-  static constexpr int B_UNITS = BN * 16;                      // 16-B weight units per LDS stage
-  static constexpr int B_IT = (B_UNITS + NTB - 1) / NTB;
   static constexpr bool OK = LDS <= LDS_CAP && MT >= 1 && NTL >= 1 && WTM % 16 == 0 && WTN % 16 == 0 &&
-                             (WTM / 16) * 16 == WTM && CK % 32 == 0 && (!GATE || NTB % HU == 0) &&
-                             B_UNITS % NTB == 0;
+                             (CK == 32 || CK == 64) && W_PIECES % 8 == 0 && WM * WN == 8;
 };
 
-template <int TH, int BN, int WM, int CK, bool GATE>
-__global__ __launch_bounds__(NTB, 2) void conv3_big_kernel(rdn_conv_desc d, int tiles_x, int tiles_y) {
-  using Cfg = BigCfg<TH, BN, WM, CK, GATE>;
-  constexpr int VEC = 8;
-  constexpr int BM = Cfg::BM, HROW = Cfg::HROW, RW = Cfg::RW, SPC = Cfg::SPC, SS = Cfg::SS;
-  constexpr int WN = Cfg::WN, WTM = Cfg::WTM, WTN = Cfg::WTN, MT = Cfg::MT, NTL = Cfg::NTL;
-  constexpr int HU = Cfg::HU, H_UNITS = Cfg::H_UNITS, H_IT = Cfg::H_IT, B_IT = Cfg::B_IT;
-  constexpr int RS = TWB + 2;                                  // halo pixels per halo row
+template <int NLO, int NHI, int SPLIT>
+__device__ __forceinline__ void wait_split(int wave) {   // vmcnt(wave < SPLIT ? NHI : NLO)
+  if (wave < SPLIT) wait_vm<NHI>();
+  else wait_vm<NLO>();
+}
+
+template <int TH, int BN, int WM, int CK, int EP>
+__global__ __launch_bounds__(NTB, 2) void conv3_big_kernel(rdn_conv_desc d, int tiles_x, int tiles_y, int nitems) {
+  using Cfg = PtCfg<TH, BN, WM, CK>;
+  constexpr int RB = Cfg::RB, RW = Cfg::RW, SPC = Cfg::SPC, SS = Cfg::SS;
+  constexpr int WTN = Cfg::WTN, MT = Cfg::MT, NTL = Cfg::NTL, W_PW = Cfg::W_PW, HP = Cfg::H_PIECES;
+  constexpr bool FWD = EP == EP_FWD || EP == EP_FWD_RES;
+  constexpr bool RES = EP == EP_FWD_RES || EP == EP_RES;
+  constexpr bool ACC = EP == EP_ACC;
   static_assert(Cfg::OK, "conv3_big geometry");
 
-  __shared__ __attribute__((aligned(16))) unsigned char lds[Cfg::LDS];
-  unsigned char* const halo = lds;
-  unsigned char* const wst = lds + Cfg::HALO_BYTES;            // two weight stages of BN x RW
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[Cfg::LDS];
+  unsigned char* const halo = lds;                               // two halo images
+  unsigned char* const wst = lds + 2 * Cfg::HALO_BYTES;          // two weight stages
+  float* const tab = (float*)(wst + 2 * Cfg::W_BYTES);           // [0, COL_MAX): bias, then slopes
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
   const int r = lane & 15, g = lane >> 4;
-  // 1-D grid, column tile fastest: the blocks reading one halo share an XCD
-  const int ncb = (d.ncols + BN - 1) / BN;
-  const int lb = xcd_remap(blockIdx.x, gridDim.x);
-  int bt = lb / ncb;
-  const int tx = bt % tiles_x;
-  bt /= tiles_x;
-  const int ty = bt % tiles_y;
-  const int nimg = bt / tiles_y;
-  const int y0 = ty * TH, x0 = tx * TWB;
-  const int n0 = (lb - (lb / ncb) * ncb) * BN;
+  const int ncb = d.ncols / BN;
   const int H = d.h, W = d.w;
   const int nch = d.cin / CK;
 
-  // ---- halo units of this thread: element offset from the halo origin, LDS offset,
-  // in-image flag; chunk c adds c * CK channels
-  const int64_t hpix0 = ((int64_t)nimg * H + (y0 - 1)) * W + (x0 - 1);
-  const bf16* const xb = (const bf16*)d.x + hpix0 * d.x_ps;
-  const bf16* const gb = GATE ? (const bf16*)d.gate + hpix0 * d.gate_ps : nullptr;
-  int hrel[H_IT], grel[GATE ? H_IT : 1], hlds[H_IT];
-  bool hok[H_IT];
-  const int hcu = (tid % HU) * VEC;   // NTB % HU == 0 for every CK used: fixed channel unit per thread
-#pragma unroll
-  for (int it = 0; it < H_IT; ++it) {
-    const int u = tid + it * NTB;
-    const int hp = u / HU;
-    const int hy = hp / RS, hx = hp - hy * RS;
-    hok[it] = u < H_UNITS && (unsigned)(y0 - 1 + hy) < (unsigned)H && (unsigned)(x0 - 1 + hx) < (unsigned)W;
-    hrel[it] = (hy * W + hx) * (int)d.x_ps;
-    if constexpr (GATE) grel[it] = (hy * W + hx) * (int)d.gate_ps;
-    hlds[it] = u < H_UNITS ? hp * HROW + (u % HU) * 16 : -1;
+  // this block's items: its XCD's contiguous share, strided by the XCD's block count
+  // (consecutive items = the column blocks of one pixel tile: one halo, one L2)
+  const int per = gridDim.x >> 3, xcd = blockIdx.x & 7;
+  const int it_lo = (int)((int64_t)nitems * xcd / 8), it_hi = (int)((int64_t)nitems * (xcd + 1) / 8);
+  int item = it_lo + (blockIdx.x >> 3);
+
+  if constexpr (FWD) {
+    for (int c = tid; c < d.ncols; c += NTB) {
+      tab[c] = d.bias[c];
+      tab[COL_MAX + c] = d.alpha[c];
+    }
   }
-  u32x4 hreg[H_IT];
-  u32x4 greg[GATE ? H_IT : 1];
-  float galpha[GATE ? VEC : 1];
-  auto load_halo = [&](int c) {
-    const int64_t co = rdn_coff(d.x_c0 + c * CK + hcu, d.x_ps, d.x_pl);
-    const int64_t cg = GATE ? rdn_coff(c * CK + hcu, d.gate_ps, d.gate_pl) : 0;
-    if constexpr (GATE) {
+
+  struct Geo { int nimg, y0, x0, n0; };
+  auto geo = [&](int itm) {
+    Geo q;
+    const int cb = itm % ncb;
+    int t = itm / ncb;
+    const int tx = t % tiles_x;
+    t /= tiles_x;
+    q.y0 = (t % tiles_y) * TH;
+    q.x0 = tx * TWB;
+    q.nimg = t / tiles_y;
+    q.n0 = cb * BN;
+    return q;
+  };
+
+  // ---- halo DMA of chunk c of item q into halo buffer hb: piece pc (wave w takes
+  // pieces w, w + 8, ...) covers image bytes pc*1024 + lane*16 -> pixel hp, physical
+  // unit pu holding logical unit hswz(pu, hx); out-of-image pixels read zeros
+  auto issue_h = [&](const Geo& q, int c, int hb) {
+    const unsigned dst = lds_addr(halo) + hb * Cfg::HALO_BYTES;
+    const bf16* const xb = (const bf16*)d.x + (((int64_t)q.nimg * H + (q.y0 - 1)) * W + (q.x0 - 1)) * d.x_ps;
 #pragma unroll
-      for (int q = 0; q < VEC; ++q) galpha[q] = d.gate_alpha[c * CK + hcu + q];
-    }
-#pragma unroll
-    for (int it = 0; it < H_IT; ++it) {
-      u32x4 v = {0u, 0u, 0u, 0u}, gv = {0u, 0u, 0u, 0u};
-      if (hok[it]) {
-        v = *(const u32x4*)(xb + hrel[it] + co);
-        if constexpr (GATE) gv = *(const u32x4*)(gb + grel[it] + cg);
-      }
-      hreg[it] = v;
-      if constexpr (GATE) greg[it] = gv;
+    for (int k = 0; k < (HP + 7) / 8; ++k) {
+      const int pc = wave + 8 * k;
+      if (pc >= HP) break;   // wave-uniform
+      const int off = pc * 1024 + lane * 16;
+      const int hp = off / RB, pu = (off % RB) / 16;
+      const int hy = hp / RS, hx = hp - (hp / RS) * RS;
+      const int u = hswz<CK>(pu, hx);
+      const bool ok =
+          hp < Cfg::HWP && (unsigned)(q.y0 - 1 + hy) < (unsigned)H && (unsigned)(q.x0 - 1 + hx) < (unsigned)W;
+      const void* src = ok ? (const void*)(xb + (int64_t)(hy * W + hx) * d.x_ps +
+                                           rdn_coff32(d.x_c0 + c * CK + u * 8, (int)d.x_ps, (int)d.x_pl))
+                           : (const void*)g_big_zero;
+      glds16(src, dst + pc * 1024);
     }
   };
-  auto store_halo = [&]() {
+  // ---- weight DMA: LDS stage (c, jj) holds K stages 2jj, 2jj+1 of chunk c (16 units
+  // = 256 B of every output column n0..n0+BN); physical unit p of row n holds logical
+  // unit p ^ (n & 15); the odd stage past a chunk's K loads zeros
+  auto issue_w = [&](int n0, int c, int jj, int wb) {
+    const unsigned dst = lds_addr(wst) + wb * Cfg::W_BYTES;
 #pragma unroll
-    for (int it = 0; it < H_IT; ++it) {
-      if (hlds[it] < 0) continue;
-      u32x4 v = hreg[it];
-      if constexpr (GATE) {
-        float dy[VEC], pr[VEC];
-        Unit16<bf16>::unpack(v, dy);
-        Unit16<bf16>::unpack(greg[it], pr);
-#pragma unroll
-        for (int q = 0; q < VEC; ++q) dy[q] = pr[q] > 0.f ? dy[q] : galpha[q] * dy[q];
-        v = Unit16<bf16>::pack(dy);
-      }
-      *(u32x4*)(halo + hlds[it]) = v;
+    for (int k = 0; k < W_PW; ++k) {
+      const int pc = wave + 8 * k;                     // piece: rows 4 pc .. 4 pc + 3
+      const int row = 4 * pc + (lane >> 4);
+      const int u = (lane & 15) ^ (row & 15);
+      const bool ok = 2 * jj + 1 < SPC || u < 8;
+      const void* src = ok ? (const void*)((const bf16*)d.wp + (int64_t)(n0 + row) * d.kp + c * Cfg::KC + jj * 128 +
+                                           u * 8)
+                           : (const void*)g_big_zero;
+      glds16(src, dst + pc * 1024);
     }
   };
 
-  // ---- weight stages: LDS stage (c, jj) holds K stages 2jj, 2jj+1 of chunk c, i.e.
-  // 16 units (256 B) of every output column n0..n0+BN
-  u32x4 wreg[B_IT];
-  const int wu = tid & 15;
-  const bf16* const wb = (const bf16*)d.wp + (int64_t)(n0 + (tid >> 4)) * d.kp + wu * VEC;
-  auto load_w = [&](int c, int jj) {
-    const bool hi_ok = 2 * jj + 1 < SPC || wu < 8;   // the odd stage past the chunk: not loaded
+  // ---- fragment addresses: lane (r, g) reads pixel column r + dx of its tile rows
+  // (k unit g of the k-step) and weight row r of its column block (unit g)
+  int a_off[CK == 64 ? 6 : 3];   // [ks][dx]: byte offset of the lane's swizzled unit
 #pragma unroll
-    for (int it = 0; it < B_IT; ++it)
-      wreg[it] = hi_ok ? *(const u32x4*)(wb + (int64_t)it * (NTB / 16) * d.kp + c * Cfg::KC + jj * 128)
-                       : u32x4{0u, 0u, 0u, 0u};
-  };
-  auto store_w = [&](int buf) {
+  for (int ks = 0; ks < (CK == 64 ? 2 : 1); ++ks)
 #pragma unroll
-    for (int it = 0; it < B_IT; ++it)
-      *(u32x4*)(wst + buf * Cfg::W_BYTES + ((tid >> 4) + it * (NTB / 16)) * RW + wu * 16) = wreg[it];
-  };
-
-  // ---- fragment addresses: per-lane bases + compile-time immediates
-  const unsigned char* const pa = halo + ((wm * MT) * RS + r) * HROW + g * 16;   // pixel frag rows
-  const int b_lane = (wn * WTN + r) * RW + g * 16;
+    for (int dx = 0; dx < 3; ++dx) a_off[ks * 3 + dx] = (r + dx) * RB + hswz<CK>(ks * 4 + g, r + dx) * 16;
+  const int a_row0 = (wm * MT) * RS * RB;
+  const int b_lane = (wn * WTN + r) * RW;
+  int b_off[4];   // per (K-stage half, k-step): swizzled unit of this lane's weight row
+#pragma unroll
+  for (int hk = 0; hk < 4; ++hk) b_off[hk] = ((hk * 4 + g) ^ r) * 16;
 
   f32x4 acc[MT][NTL];
+  auto zero_acc = [&]() {
 #pragma unroll
-  for (int i = 0; i < MT; ++i)
+    for (int i = 0; i < MT; ++i)
 #pragma unroll
-    for (int jn = 0; jn < NTL; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int jn = 0; jn < NTL; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
 
-  // K stage j (64 deep) of the current chunk, from weight buffer pbs (+h*128 B)
-  auto compute = [&](auto JJ, const unsigned char* pbs) {
-    constexpr int jj = decltype(JJ)::value;
+  // LDS stage jj of a chunk (K stages 2jj, 2jj+1) from halo image ph, weights pbs
+  auto compute = [&](int jj, const unsigned char* ph, const unsigned char* pbs) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int j = 2 * jj + h;
@@ -200,13 +224,15 @@ __global__ __launch_bounds__(NTB, 2) void conv3_big_kernel(rdn_conv_desc d, int 
       for (int ks = 0; ks < 2; ++ks) {
         const int k0 = j * 64 + ks * 32;
         if (k0 >= 9 * CK) break;               // padded K: zero weights, skipped
-        const int tap = k0 / CK, ci = k0 - (k0 / CK) * CK;
-        const int ao = ((tap / 3) * RS + tap % 3) * HROW + ci * 2;
+        const int tap = k0 / CK, ksub = (k0 - tap * CK) / 32;
+        const int dy = tap / 3, dx = tap % 3;
+        const unsigned char* pa = ph + a_row0 + dy * RS * RB + a_off[ksub * 3 + dx];
+        __builtin_amdgcn_sched_barrier(0);   // k-steps stay apart: one fragment set live at a time
         u32x4 af[MT], bfr[NTL];
 #pragma unroll
-        for (int i = 0; i < MT; ++i) af[i] = *(const u32x4*)(pa + ao + i * RS * HROW);
+        for (int i = 0; i < MT; ++i) af[i] = *(const u32x4*)(pa + i * RS * RB);
 #pragma unroll
-        for (int jn = 0; jn < NTL; ++jn) bfr[jn] = *(const u32x4*)(pbs + jn * 16 * RW + h * 128 + ks * 64);
+        for (int jn = 0; jn < NTL; ++jn) bfr[jn] = *(const u32x4*)(pbs + jn * 16 * RW + b_off[2 * h + ks]);
 #pragma unroll
         for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -218,115 +244,126 @@ __global__ __launch_bounds__(NTB, 2) void conv3_big_kernel(rdn_conv_desc d, int 
     }
   };
 
-  load_halo(0);
-  load_w(0, 0);
-  store_halo();
-  store_w(0);
-  __syncthreads();
-  int buf = 0;
-  for (int c = 0; c < nch; ++c) {
-    const bool more = c + 1 < nch;
-    if (more) load_halo(c + 1);   // in flight during this chunk's stages
-    auto stage = [&](auto JJ) {
-      constexpr int jj = decltype(JJ)::value;
-      const bool nxt = jj + 1 < SS || more;
-      if (nxt) load_w(jj + 1 < SS ? c : c + 1, jj + 1 < SS ? jj + 1 : 0);
-      compute(JJ, wst + buf * Cfg::W_BYTES + b_lane);
-      if (nxt) store_w(buf ^ 1);
-      __syncthreads();
-      buf ^= 1;
-    };
-    static_for<SS>(stage);
-    if (more) {
-      store_halo();
-      __syncthreads();
-    }
-  }
-
-  // ---- epilogue: fp32 tile [BM pixels][BN columns] through LDS, then 16-B NHWC units
-  constexpr int CROW = Cfg::CROW;
-  {
-    unsigned char* const ct = lds;
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
+  // ---- epilogue: straight from the accumulators, through buffer descriptors on the
+  // item's first pixel (32-bit offsets: few registers; pixels past the image edge get
+  // the OOB offset, so loads read zeros and stores are dropped, no branches).  Lane
+  // (r, g) of fragment (i, jn) holds channels cl..cl+3 of tile pixel (row wm*MT + i,
+  // column r): one 8-byte unit per operand.
+  u32x2 eop[(RES || ACC) ? MT : 1][(RES || ACC) ? NTL : 1];
+  auto epilogue = [&](const Geo& q) {
+    const int64_t pix0 = ((int64_t)q.nimg * H + q.y0) * W + q.x0;
+    const __amdgpu_buffer_rsrc_t ro = rdn_rsrc((const bf16*)d.out + pix0 * d.out_ps);
+    const int ops = (int)d.out_ps, pps = (int)d.pre_ps;
+    const bool col_ok = q.x0 + r < W;
+    if constexpr (RES || ACC) {   // operands first: their latency overlaps the loop below
+      const int eps = RES ? (int)d.res_ps : ops;
+      const __amdgpu_buffer_rsrc_t re = RES ? rdn_rsrc((const bf16*)d.res + pix0 * d.res_ps) : ro;
 #pragma unroll
       for (int jn = 0; jn < NTL; ++jn) {
-        const int p = (wm * MT + i) * 16 + r;
-        const int c = wn * WTN + jn * 16 + g * 4;
-        *(f32x4*)(ct + p * CROW + c * 4) = acc[i][jn];
+        const int cl = q.n0 + wn * WTN + jn * 16 + g * 4;
+        const int coff =
+            RES ? rdn_coff32(d.res_c0 + cl, eps, (int)d.res_pl) : rdn_coff32(d.out_c0 + cl, ops, (int)d.out_pl);
+        const bool cok = col_ok & (RES ? cl < d.res_climit : true);
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+          const bool ok = cok & (q.y0 + wm * MT + i < H);
+          eop[i][jn] = rdn_ld8(re, ok, (((wm * MT + i) * W + r) * eps + coff) * 2);
+        }
       }
-  }
-  __syncthreads();
-  const float* const Ct = (const float*)lds;
-  const int flags = d.flags;
-  const bool fast = (d.ncols % VEC) == 0 && !(flags & RDN_EPI_OUT_NCHW) && y0 + TH <= H && x0 + TWB <= W &&
-                    (!(flags & RDN_EPI_RESID) || (d.res_climit % VEC == 0 && d.res_ps % VEC == 0 &&
-                                                  d.res_c0 % VEC == 0)) &&
-                    d.out_ps % VEC == 0 && d.out_c0 % VEC == 0 && d.pre_ps % VEC == 0;
-  if (!fast) {
-    c3::store_tile<bf16, BN, NTB>(d, Ct, CROW / 4, y0, x0, nimg, n0, tid);
-    return;
-  }
-  constexpr int UPR = BN / VEC, EU = BM * UPR, E_IT = (EU + NTB - 1) / NTB;
-  constexpr bool COLFIX = NTB % UPR == 0;   // a thread's output channels are fixed
-  const int64_t opix0 = ((int64_t)nimg * H + y0) * W + x0;
-  float ebias[VEC], ealpha[VEC];
-  int64_t cf_pre = 0, cf_out = 0, cf_res = 0;
-  auto col_consts = [&](int c) {
-#pragma unroll
-    for (int q = 0; q < VEC; ++q) {
-      ebias[q] = (flags & RDN_EPI_BIAS) ? d.bias[c + q] : 0.f;
-      ealpha[q] = (flags & RDN_EPI_PRELU) ? d.alpha[c + q] : 0.f;
     }
-    cf_pre = rdn_coff(c, d.pre_ps, d.pre_pl);
-    cf_out = rdn_coff(d.out_c0 + c, d.out_ps, d.out_pl);
-    cf_res = rdn_coff(d.res_c0 + c, d.res_ps, d.res_pl);
+    const __amdgpu_buffer_rsrc_t rp = FWD ? rdn_rsrc((const bf16*)d.pre + pix0 * d.pre_ps) : ro;
+#pragma unroll
+    for (int jn = 0; jn < NTL; ++jn) {
+      const int cl = q.n0 + wn * WTN + jn * 16 + g * 4;
+      f32x4 bias = {0.f, 0.f, 0.f, 0.f}, alpha = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (FWD) {
+        bias = *(const f32x4*)(tab + cl);
+        alpha = *(const f32x4*)(tab + COL_MAX + cl);
+      }
+      const int co = rdn_coff32(d.out_c0 + cl, ops, (int)d.out_pl);
+      const int cp = FWD ? rdn_coff32(cl, pps, (int)d.pre_pl) : 0;
+      const bool res_ok = RES ? cl < d.res_climit : true;
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const bool ok = col_ok & (q.y0 + wm * MT + i < H);
+        const int prow = (wm * MT + i) * W + r;   // pixel relative to the item origin
+        float v[4] = {acc[i][jn][0], acc[i][jn][1], acc[i][jn][2], acc[i][jn][3]};
+        if constexpr (FWD) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += bias[e];
+          int o = ok ? (prow * pps + cp) * 2 : RDN_OOB;
+          asm volatile("" : "+v"(o));
+          __builtin_amdgcn_raw_buffer_store_b64(rdn_pack4(v), rp, o, 0, 0);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : alpha[e] * v[e];
+        }
+        if constexpr (RES || ACC) {
+          if (res_ok) {
+            v[0] += bf16lo(eop[i][jn][0]); v[1] += bf16hi(eop[i][jn][0]);
+            v[2] += bf16lo(eop[i][jn][1]); v[3] += bf16hi(eop[i][jn][1]);
+          }
+        }
+        int o = ok ? (prow * ops + co) * 2 : RDN_OOB;
+        asm volatile("" : "+v"(o));
+        __builtin_amdgcn_raw_buffer_store_b64(rdn_pack4(v), ro, o, 0, 0);
+      }
+    }
   };
-  if constexpr (COLFIX) col_consts(n0 + (tid % UPR) * VEC);
+
+  // ---- prologue: first item's chunk-0 halo and first weight stage
+  Geo cur = geo(item < it_hi ? item : it_lo);
+  if (item < it_hi) {
+    issue_w(cur.n0, 0, 0, 0);
+    issue_h(cur, 0, 0);
+  }
+  wait_vm<0>();
+  __syncthreads();   // slopes / biases, first halo and weights
+  // Per LDS stage: issue the NEXT weight stage (into the buffer every wave finished
+  // reading before the last barrier) and, at a chunk's first stage, the next chunk's
+  // halo (into the other halo buffer, free since the chunk boundary's barrier), then
+  // compute; each wave then waits for its own weight DMA of the next stage -- the
+  // halo DMA issued after it stays in flight one more stage -- and a barrier
+  // publishes the stage.  Epilogue stores go out right after the item's last barrier
+  // and are retired by the next stage's wait.
+  int wbuf = 0, hbuf = 0;
+  while (item < it_hi) {
+    const int nxt_item = item + per;
+    const bool has_next = nxt_item < it_hi;
+    const Geo nq = geo(has_next ? nxt_item : item);
+    zero_acc();
+    for (int c = 0; c < nch; ++c) {
+      const bool more = c + 1 < nch;
+      const unsigned char* const ph = halo + hbuf * Cfg::HALO_BYTES;
 #pragma unroll
-  for (int it = 0; it < E_IT; ++it) {
-    const int u = tid + it * NTB;
-    if (EU % NTB && u >= EU) break;
-    const int px = u / UPR, cl = (u - px * UPR) * VEC, c = n0 + cl;
-    if constexpr (!COLFIX) col_consts(c);
-    float v[VEC];
-    const float* src = Ct + (px * CROW) / 4 + cl;
-    const f32x4 t0 = *(const f32x4*)src, t1 = *(const f32x4*)(src + 4);
-    v[0] = t0[0]; v[1] = t0[1]; v[2] = t0[2]; v[3] = t0[3];
-    v[4] = t1[0]; v[5] = t1[1]; v[6] = t1[2]; v[7] = t1[3];
-    const int64_t opix = opix0 + (px / TWB) * W + px % TWB;
-#pragma unroll
-    for (int q = 0; q < VEC; ++q) v[q] += ebias[q];
-    if (flags & RDN_EPI_STORE_PRE) *(u32x4*)((bf16*)d.pre + opix * d.pre_ps + cf_pre) = Unit16<bf16>::pack(v);
-    if (flags & RDN_EPI_PRELU) {
-#pragma unroll
-      for (int q = 0; q < VEC; ++q) v[q] = v[q] > 0.f ? v[q] : ealpha[q] * v[q];
+      for (int jj = 0; jj < SS; ++jj) {
+        const bool nxt = jj + 1 < SS || more || has_next;
+        if (nxt) {
+          if (jj + 1 < SS) issue_w(cur.n0, c, jj + 1, wbuf ^ 1);
+          else if (more) issue_w(cur.n0, c + 1, 0, wbuf ^ 1);
+          else issue_w(nq.n0, 0, 0, wbuf ^ 1);
+        }
+        const bool hl = jj == 0 && (more || has_next);
+        if (hl) issue_h(more ? cur : nq, more ? c + 1 : 0, hbuf ^ 1);
+        compute(jj, ph, wst + wbuf * Cfg::W_BYTES + b_lane);
+        if (hl && SS > 1) wait_split<HP / 8, HP / 8 + 1, HP % 8>(wave);   // weights landed; halo may fly
+        else wait_vm<0>();
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        wbuf ^= 1;
+      }
+      hbuf ^= 1;
     }
-    bf16* const op = (bf16*)d.out + opix * d.out_ps + cf_out;
-    float rv[VEC];
-    if ((flags & RDN_EPI_RESID) && c < d.res_climit) {
-      Unit16<bf16>::unpack(*(const u32x4*)((const bf16*)d.res + opix * d.res_ps + cf_res), rv);
-#pragma unroll
-      for (int q = 0; q < VEC; ++q) v[q] += rv[q];
-    }
-    if (flags & RDN_EPI_ACCUM) {
-      Unit16<bf16>::unpack(*(const u32x4*)op, rv);
-#pragma unroll
-      for (int q = 0; q < VEC; ++q) v[q] += rv[q];
-    }
-    *(u32x4*)op = Unit16<bf16>::pack(v);
+    epilogue(cur);   // global stores drain under the next item
+    item = nxt_item;
+    cur = nq;
   }
 }
 
 int big_mode() {
-  // RDN_BIG: unset/"1" = the default shape rule below; "0" = never (conv3_halo);
-  // "all" = every bf16 shape the kernel can take (experiments)
+  // RDN_BIG: unset/"1" = the default shape rule below; "0" = never (conv3_halo)
   static const int m = [] {
     const char* e = getenv("RDN_BIG");
-    if (!e) return 1;
-    if (e[0] == '0') return 0;
-    if (e[0] == 'a') return 2;
-    return 1;
+    return (e && e[0] == '0') ? 0 : 1;
   }();
   return m;
 }
@@ -342,122 +379,101 @@ int cu_count() {
   return cus;
 }
 
+int epi_mode(const rdn_conv_desc* d) {
+  const int f = d->flags;
+  const int fwd = RDN_EPI_BIAS | RDN_EPI_PRELU | RDN_EPI_STORE_PRE;
+  if (f == fwd) return EP_FWD;
+  if (f == (fwd | RDN_EPI_RESID)) return EP_FWD_RES;
+  if (f == 0) return EP_PLAIN;
+  if (f == RDN_EPI_ACCUM) return EP_ACC;
+  if (f == RDN_EPI_RESID) return EP_RES;
+  return -1;
+}
+
+template <int TH, int BN, int WM, int CK, int EP>
+int launch_pt(const rdn_conv_desc* d, hipStream_t st, int tiles_x, int tiles_y, int nitems) {
+  if constexpr (!PtCfg<TH, BN, WM, CK>::OK) {
+    return 1;
+  } else {
+    RDN_PROBE("conv3_big_kernel<bf16,%d,%d,%d,%d>", TH, BN, WM, CK);
+    const int per_xcd = (nitems + 7) / 8;
+    int slots = cu_count() / 8;
+    if (slots > per_xcd) slots = per_xcd;
+    if (slots < 1) slots = 1;
+    hipLaunchKernelGGL((conv3_big_kernel<TH, BN, WM, CK, EP>), dim3((unsigned)(8 * slots)), dim3(NTB), 0, st, *d,
+                       tiles_x, tiles_y, nitems);
+    return rdn_check_launch("rdn_conv_fwd(conv3 big)");
+  }
+}
+
 template <int TH, int BN, int WM, int CK>
 int launch_big(const rdn_conv_desc* d, hipStream_t st) {
-  constexpr bool OKP = BigCfg<TH, BN, WM, CK, false>::OK, OKG = BigCfg<TH, BN, WM, CK, true>::OK;
   const int tiles_x = (d->w + TWB - 1) / TWB, tiles_y = (d->h + TH - 1) / TH;
-  const int64_t blocks = (int64_t)d->n * tiles_x * tiles_y * ((d->ncols + BN - 1) / BN);
-  if (blocks >= (1ll << 31)) return 1;
-  if (d->gate) {
-    if constexpr (OKG) {
-      RDN_PROBE("conv3_big_kernel<bf16,%d,%d,%d,%d,gate>", TH, BN, WM, CK);
-      conv3_big_kernel<TH, BN, WM, CK, true><<<dim3((unsigned)blocks), NTB, 0, st>>>(*d, tiles_x, tiles_y);
-      return rdn_check_launch("rdn_conv_fwd(conv3 big)");
-    }
-    return 1;
-  }
-  if constexpr (OKP) {
-    RDN_PROBE("conv3_big_kernel<bf16,%d,%d,%d,%d>", TH, BN, WM, CK);
-    conv3_big_kernel<TH, BN, WM, CK, false><<<dim3((unsigned)blocks), NTB, 0, st>>>(*d, tiles_x, tiles_y);
-    return rdn_check_launch("rdn_conv_fwd(conv3 big)");
+  const int64_t nitems = (int64_t)d->n * tiles_x * tiles_y * (d->ncols / BN);
+  if (nitems >= (1ll << 31)) return 1;
+  const int ni = (int)nitems;
+  switch (epi_mode(d)) {
+    case EP_FWD: return launch_pt<TH, BN, WM, CK, EP_FWD>(d, st, tiles_x, tiles_y, ni);
+    case EP_FWD_RES: return launch_pt<TH, BN, WM, CK, EP_FWD_RES>(d, st, tiles_x, tiles_y, ni);
+    case EP_PLAIN: return launch_pt<TH, BN, WM, CK, EP_PLAIN>(d, st, tiles_x, tiles_y, ni);
+    case EP_ACC: return launch_pt<TH, BN, WM, CK, EP_ACC>(d, st, tiles_x, tiles_y, ni);
+    case EP_RES: return launch_pt<TH, BN, WM, CK, EP_RES>(d, st, tiles_x, tiles_y, ni);
   }
   return 1;
 }
 
-template <int TH, int BN, int WM, int CK, bool GATE>
-int blocks_per_cu() {
-  static const int n = [] {
-    int v = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, conv3_big_kernel<TH, BN, WM, CK, GATE>, NTB, 0) !=
-            hipSuccess || v < 1)
-      v = 1;
-    return v;
-  }();
-  return n;
-}
-
-// Candidate tiles (TH x 16 pixels x BN columns, WM waves along the pixels) and a
-// per-block efficiency weight (larger wave tiles: more MFMAs per fragment read)
-struct Plan { int th, bn, wm; double eff; };
-constexpr Plan kPlans[] = {{16, 128, 4, 1.0}, {16, 96, 4, 0.95}, {16, 64, 4, 0.85},
-                           {8, 160, 4, 0.9}, {8, 128, 2, 0.85}, {8, 64, 2, 0.7}};
-constexpr int kNPlans = sizeof(kPlans) / sizeof(kPlans[0]);
-
-template <int I, int CK>
-int launch_plan(const rdn_conv_desc* d, hipStream_t st) {
-  constexpr Plan p = kPlans[I];
-  return launch_big<p.th, p.bn, p.wm, CK>(d, st);
-}
-
-template <int I, int CK>
-int plan_bpc(bool gate) {
-  constexpr Plan p = kPlans[I];
-  if constexpr (BigCfg<p.th, p.bn, p.wm, CK, true>::OK) {
-    if (gate) return blocks_per_cu<p.th, p.bn, p.wm, CK, true>();
-  }
-  if constexpr (BigCfg<p.th, p.bn, p.wm, CK, false>::OK) {
-    if (!gate) return blocks_per_cu<p.th, p.bn, p.wm, CK, false>();
-  }
-  return 0;   // not instantiable
-}
-
-template <int CK, int... I>
-void fill_bpc(int* bpc, bool gate, std::integer_sequence<int, I...>) {
-  ((bpc[I] = plan_bpc<I, CK>(gate)), ...);
-}
-
-// tile plan: the candidate minimising (rounds of blocks over the resident slots) x
-// (per-block cost), exact column tiling only
+// Where the persistent kernel wins (per-layer A/B against conv3_halo on the train
+// step's own launches, B16 and B32, profiles/r03_v3_big_vs_halo.json):
+// * 128-column items (64 x 64 wave tiles) when the items spread evenly over the CUs
+//   (the last round >= 90 % full: one item more on some CUs is a whole item of tail,
+//   where conv3_halo's 128-pixel tiles at 2-3 blocks per CU balance finer) and each
+//   item runs >= 2 channel chunks (one chunk leaves the next halo's load exposed);
+// * 64-column items (64 x 32 wave tiles, LDS-read heavier) only with >= 8 chunk
+//   iterations per CU, where the cross-item prefetch carries it.
 template <int CK>
 int big_dispatch(const rdn_conv_desc* d, hipStream_t st) {
-  const int cus = cu_count();
-  const bool gate = d->gate != nullptr;
-  int bpc[kNPlans];
-  fill_bpc<CK>(bpc, gate, std::make_integer_sequence<int, kNPlans>{});
-  int best = -1;
-  double best_t = 1e30;
-  for (int i = 0; i < kNPlans; ++i) {
-    const Plan& p = kPlans[i];
-    if (!bpc[i] || d->ncols % p.bn) continue;
-    const int64_t tiles = (int64_t)d->n * ((d->h + p.th - 1) / p.th) * ((d->w + TWB - 1) / TWB);
-    const int64_t blocks = tiles * (d->ncols / p.bn);
-    const int64_t slots = (int64_t)cus * bpc[i];
-    const double rounds = (double)((blocks + slots - 1) / slots);
-    const double per_block = (double)p.th * p.bn / (16.0 * 128.0) / p.eff / bpc[i];
-    const double t = rounds * per_block;
-    if (t < best_t - 1e-9) { best_t = t; best = i; }
+  const int64_t tiles = (int64_t)d->n * ((d->h + 15) / 16) * ((d->w + 15) / 16);
+  const int cus = cu_count(), nch = d->cin / CK;
+  auto even = [&](int64_t items) {
+    const int64_t rounds = (items + cus - 1) / cus;
+    return items * 10 >= rounds * cus * 9;
+  };
+  if (d->ncols % 128 == 0) {
+    const int64_t items = tiles * (d->ncols / 128);
+    if (nch >= 2 && items >= cus && even(items)) return launch_big<16, 128, 4, CK>(d, st);
+    return 1;
   }
-  switch (best) {
-    case 0: return launch_plan<0, CK>(d, st);
-    case 1: return launch_plan<1, CK>(d, st);
-    case 2: return launch_plan<2, CK>(d, st);
-    case 3: return launch_plan<3, CK>(d, st);
-    case 4: return launch_plan<4, CK>(d, st);
-    case 5: return launch_plan<5, CK>(d, st);
-  }
+  const int64_t items = tiles * (d->ncols / 64);
+  if (items * nch >= 8ll * cus && even(items)) return launch_big<16, 64, 4, CK>(d, st);
   return 1;
 }
 
 }  // namespace
 
 // Level 1-3 bf16 3x3 convs with enough columns and input channels for the large
-// tile (else 1: the caller falls back to conv3_ws / conv3_halo)
+// tile (else 1: the caller falls back to conv3_wsd / conv3_ws / conv3_halo)
 int rdn_conv3_big_launch(const rdn_conv_desc* d, int ck, hipStream_t st) {
-  const int mode = big_mode();
-  if (!mode || d->dtype != RDN_BF16 || d->gather != RDN_G_CONV3) return 1;
-  if (d->bn || d->bm) return 1;
-  if (ck != 32 && ck != 64) return 1;
-  if (d->gate && (d->gate_ps % 8 || ((uintptr_t)d->gate & 15) || !d->gate_alpha)) return 1;
-  if (d->ncols % 32 || d->ncols < 64 || d->cin < 64) return 1;
+  if (!big_mode() || d->dtype != RDN_BF16 || d->gather != RDN_G_CONV3) return 1;
+  if (d->bn || d->bm || d->gate) return 1;
+  if (ck != 64) return 1;   // 32-channel chunks: conv3_halo measured faster (level-1 conv_3, r03)
+  if (epi_mode(d) < 0) return 1;
+  if (d->ncols % 64 || d->ncols < 64 || d->cin < 64 || d->ncols > COL_MAX) return 1;
   if (d->x_ps % 8 || d->x_c0 % 8 || ((uintptr_t)d->x & 15) || ((uintptr_t)d->wp & 15) || d->kp % 8) return 1;
-  if (mode == 1) {
-    // default rule: grids of at least one block per CU at the 16 x 16 x 128 tile
-    // (levels 1-3 of the 256^2 train step and larger)
-    const int64_t px = (int64_t)d->n * d->h * d->w;
-    if (px < 8192) return 1;
-  }
-  // per-thread halo offsets in 32 bits
-  if ((int64_t)18 * d->w * d->x_ps >= (1ll << 30) || (d->gate && (int64_t)18 * d->w * d->gate_ps >= (1ll << 30)))
+  if (d->out_ps % 4 || d->out_c0 % 4 || ((uintptr_t)d->out & 7)) return 1;
+  if ((d->flags & RDN_EPI_STORE_PRE) && (d->pre_ps % 4 || ((uintptr_t)d->pre & 7))) return 1;
+  if ((d->flags & RDN_EPI_RESID) && (d->res_ps % 4 || d->res_c0 % 4 || d->res_climit % 4 || ((uintptr_t)d->res & 7)))
     return 1;
-  return ck == 64 ? big_dispatch<64>(d, st) : big_dispatch<32>(d, st);
+  // grids of at least one item per CU at the 16 x 16 x 128 tile (levels 1-3 of the
+  // 256^2 train step and larger)
+  const int64_t px = (int64_t)d->n * d->h * d->w;
+  if (px < 8192) return 1;
+  // 32-bit element offsets (halo) and byte offsets (epilogue, from a per-item base)
+  auto fits = [&](int64_t ps, int64_t pl, int c_hi) {
+    return 2 * ((int64_t)(18 + 1) * d->w * ps + rdn_coff(c_hi, ps, pl)) < (int64_t)RDN_OOB - 16;
+  };
+  if (!fits(d->x_ps, d->x_pl, d->x_c0 + d->cin) || !fits(d->out_ps, d->out_pl, d->out_c0 + d->ncols) ||
+      ((d->flags & RDN_EPI_STORE_PRE) && !fits(d->pre_ps, d->pre_pl, d->ncols)) ||
+      ((d->flags & RDN_EPI_RESID) && !fits(d->res_ps, d->res_pl, d->res_c0 + d->res_climit)))
+    return 1;
+  return big_dispatch<64>(d, st);
 }
