@@ -88,14 +88,14 @@ struct PtCfg {
   static constexpr int RW = 256;                                // LDS weight row: 2 x 128 B
   static constexpr int W_BYTES = BN * RW;
   static constexpr int W_PIECES = W_BYTES / 1024;
-  static constexpr int W_PW = W_PIECES / 8;                     // weight pieces per wave per stage
+  static constexpr int W_PW = (W_PIECES + 7) / 8;               // weight pieces per wave per stage (max)
   static constexpr int TAB = 2 * COL_MAX * 4;
   static constexpr int LDS = 2 * HALO_BYTES + 2 * W_BYTES + TAB;
   static constexpr int WN = 8 / WM;
   static constexpr int WTM = BM / WM, WTN = BN / WN;            // wave tile (pixels x columns)
   static constexpr int MT = WTM / 16, NTL = WTN / 16;
   static constexpr bool OK = LDS <= LDS_CAP && MT >= 1 && NTL >= 1 && WTM % 16 == 0 && WTN % 16 == 0 &&
-                             (CK == 32 || CK == 64) && W_PIECES % 8 == 0 && WM * WN == 8;
+                             (CK == 32 || CK == 64) && WM * WN == 8;
 };
 
 template <int NLO, int NHI, int SPLIT>
@@ -183,6 +183,7 @@ __global__ __launch_bounds__(NTB, 2) void conv3_big_kernel(rdn_conv_desc d, int 
 #pragma unroll
     for (int k = 0; k < W_PW; ++k) {
       const int pc = wave + 8 * k;                     // piece: rows 4 pc .. 4 pc + 3
+      if (pc >= Cfg::W_PIECES) break;                  // wave-uniform
       const int row = 4 * pc + (lane >> 4);
       const int u = (lane & 15) ^ (row & 15);
       const bool ok = 2 * jj + 1 < SPC || u < 8;
@@ -424,27 +425,41 @@ int launch_big(const rdn_conv_desc* d, hipStream_t st) {
 
 // Where the persistent kernel wins (per-layer A/B against conv3_halo on the train
 // step's own launches, B16 and B32, profiles/r03_v3_big_vs_halo.json):
-// * 128-column items (64 x 64 wave tiles) when the items spread evenly over the CUs
-//   (the last round >= 90 % full: one item more on some CUs is a whole item of tail,
-//   where conv3_halo's 128-pixel tiles at 2-3 blocks per CU balance finer) and each
-//   item runs >= 2 channel chunks (one chunk leaves the next halo's load exposed);
-// * 64-column items (64 x 32 wave tiles, LDS-read heavier) only with >= 8 chunk
-//   iterations per CU, where the cross-item prefetch carries it.
+// * items spread evenly over the CUs (the last round >= 90 % full: one item more on
+//   some CUs is a whole item of tail, where conv3_halo's 128-pixel tiles at 2-3
+//   blocks per CU balance finer);
+// * 128 / 96-column items (64 x 64 / 64 x 48 wave tiles) with >= 2 channel chunks
+//   per item, or >= 4 items per CU on >= 128 x 128 images (with one chunk and one
+//   item per CU the next halo's load is exposed); 80 / 64-column items (32 x 80 /
+//   64 x 32 wave tiles, LDS-read heavier) with >= 8 chunk iterations per CU on
+//   >= 128 x 128 images, where the cross-item prefetch carries them (the level-1
+//   input gradients: 20-35 % faster than conv3_halo, up_0's 1.6x);
+// * 32-channel chunks only for single-chunk input gradients (a 5-chunk 160-channel
+//   forward measured slower than conv3_halo).
 template <int CK>
 int big_dispatch(const rdn_conv_desc* d, hipStream_t st) {
   const int64_t tiles = (int64_t)d->n * ((d->h + 15) / 16) * ((d->w + 15) / 16);
   const int cus = cu_count(), nch = d->cin / CK;
+  if (CK == 32 && nch != 1) return 1;
   auto even = [&](int64_t items) {
     const int64_t rounds = (items + cus - 1) / cus;
-    return items * 10 >= rounds * cus * 9;
+    return items >= cus && items * 10 >= rounds * cus * 9;
   };
-  if (d->ncols % 128 == 0) {
-    const int64_t items = tiles * (d->ncols / 128);
-    if (nch >= 2 && items >= cus && even(items)) return launch_big<16, 128, 4, CK>(d, st);
-    return 1;
-  }
-  const int64_t items = tiles * (d->ncols / 64);
-  if (items * nch >= 8ll * cus && even(items)) return launch_big<16, 64, 4, CK>(d, st);
+  // single-chunk and narrow-column launches won on the >= 128 x 128 images (level 1,
+  // up_0) and lost on level 2's 64 x 64 ones (r03 per-layer A/B)
+  const bool big_img = (int64_t)d->h * d->w >= 128 * 128;
+  auto wide_ok = [&](int bn) {
+    const int64_t items = tiles * (d->ncols / bn);
+    return even(items) && (nch >= 2 || (items >= 4ll * cus && big_img));
+  };
+  auto narrow_ok = [&](int bn) {
+    const int64_t items = tiles * (d->ncols / bn);
+    return even(items) && items * nch >= 8ll * cus && big_img;
+  };
+  if (d->ncols % 128 == 0) return wide_ok(128) ? launch_big<16, 128, 4, CK>(d, st) : 1;
+  if (d->ncols % 96 == 0) return wide_ok(96) ? launch_big<16, 96, 4, CK>(d, st) : 1;
+  if (d->ncols % 80 == 0) return narrow_ok(80) ? launch_big<16, 80, 8, CK>(d, st) : 1;
+  if (d->ncols % 64 == 0) return narrow_ok(64) ? launch_big<16, 64, 4, CK>(d, st) : 1;
   return 1;
 }
 
@@ -455,9 +470,9 @@ int big_dispatch(const rdn_conv_desc* d, hipStream_t st) {
 int rdn_conv3_big_launch(const rdn_conv_desc* d, int ck, hipStream_t st) {
   if (!big_mode() || d->dtype != RDN_BF16 || d->gather != RDN_G_CONV3) return 1;
   if (d->bn || d->bm || d->gate) return 1;
-  if (ck != 64) return 1;   // 32-channel chunks: conv3_halo measured faster (level-1 conv_3, r03)
+  if (ck != 32 && ck != 64) return 1;
   if (epi_mode(d) < 0) return 1;
-  if (d->ncols % 64 || d->ncols < 64 || d->cin < 64 || d->ncols > COL_MAX) return 1;
+  if (d->ncols % 16 || d->ncols < 64 || d->cin < 32 || d->ncols > COL_MAX) return 1;
   if (d->x_ps % 8 || d->x_c0 % 8 || ((uintptr_t)d->x & 15) || ((uintptr_t)d->wp & 15) || d->kp % 8) return 1;
   if (d->out_ps % 4 || d->out_c0 % 4 || ((uintptr_t)d->out & 7)) return 1;
   if ((d->flags & RDN_EPI_STORE_PRE) && (d->pre_ps % 4 || ((uintptr_t)d->pre & 7))) return 1;
@@ -475,5 +490,5 @@ int rdn_conv3_big_launch(const rdn_conv_desc* d, int ck, hipStream_t st) {
       ((d->flags & RDN_EPI_STORE_PRE) && !fits(d->pre_ps, d->pre_pl, d->ncols)) ||
       ((d->flags & RDN_EPI_RESID) && !fits(d->res_ps, d->res_pl, d->res_c0 + d->res_climit)))
     return 1;
-  return big_dispatch<64>(d, st);
+  return ck == 64 ? big_dispatch<64>(d, st) : big_dispatch<32>(d, st);
 }
