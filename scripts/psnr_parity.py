@@ -134,7 +134,7 @@ def run_gpu(args, params, data, dtype):
     with torch.no_grad():
         den = torch.cat([model.improved_sampling(ev_noisy[i:i + args.eval_batch].to(dev)).cpu()
                          for i in range(0, ev_noisy.size(0), args.eval_batch)])
-    losses = [float(v) for v in torch.stack(losses).cpu()]
+    losses = [float(v) for v in torch.stack(losses).detach().cpu()]
     return {"psnr": psnr_per_image(den, ev_clean), "loss_first": losses[0], "loss_last": losses[-1],
             "train_s": round(t_train, 2), "losses": losses,
             "_state": {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}}
