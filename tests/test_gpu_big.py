@@ -77,6 +77,8 @@ CASES = [
     ("L1_conv2_dgrad_ck32_accum", 16, 128, 128, 32, 32, 0, 0, 128, 128, 0, 32, None, False, True),
     ("L1_conv3_dgrad_bn80_resid", 16, 128, 128, 64, 64, 0, 0, 160, 160, 0, 32, (160, 0, 64), False, False),
     ("L1_conv1_dgrad_bn96_accum", 16, 128, 128, 32, 32, 0, 0, 96, 96, 0, 32, None, False, True),
+    ("L1_conv2_fwd_bn32_planar", 16, 128, 128, 128, 160, 0, 32, 32, 160, 128, 32, None, False, False),
+    ("L1_conv0_fwd_bn32_planar", 16, 128, 128, 64, 160, 0, 32, 32, 160, 64, 32, None, False, False),
 ]
 # gated input gradients are not taken by conv3_big (they stay on conv3_halo)
 GATED = ("L3_gated_dgrad", 8, 32, 32, 256, 256, 0, 0, 640, 640, 0, 128, None, True, True)

@@ -460,6 +460,16 @@ int big_dispatch(const rdn_conv_desc* d, hipStream_t st) {
   if (d->ncols % 96 == 0) return wide_ok(96) ? launch_big<16, 96, 4, CK>(d, st) : 1;
   if (d->ncols % 80 == 0) return narrow_ok(80) ? launch_big<16, 80, 8, CK>(d, st) : 1;
   if (d->ncols % 64 == 0) return narrow_ok(64) ? launch_big<16, 64, 4, CK>(d, st) : 1;
+  if (d->ncols == 32) {
+    // the narrow level-1 forwards (64 / 128 input channels -> 32; 32 x 32 wave tiles,
+    // near the HBM ridge): per-layer A/B at B16, conv_0 28 -> 26 us (was conv3_wsd),
+    // conv_2 41 -> 36.5 us (was conv3_halo); the 32-channel level-0 ones are a tie
+    // with conv3_ws and stay there
+    if constexpr (CK == 64) {
+      const int64_t items = tiles;
+      return (even(items) && items >= 4ll * cus && big_img) ? launch_big<16, 32, 8, CK>(d, st) : 1;
+    }
+  }
   return 1;
 }
 
@@ -472,7 +482,7 @@ int rdn_conv3_big_launch(const rdn_conv_desc* d, int ck, hipStream_t st) {
   if (d->bn || d->bm || d->gate) return 1;
   if (ck != 32 && ck != 64) return 1;
   if (epi_mode(d) < 0) return 1;
-  if (d->ncols % 16 || d->ncols < 64 || d->cin < 32 || d->ncols > COL_MAX) return 1;
+  if (d->ncols % 16 || d->ncols < 32 || d->cin < 32 || d->ncols > COL_MAX) return 1;
   if (d->x_ps % 8 || d->x_c0 % 8 || ((uintptr_t)d->x & 15) || ((uintptr_t)d->wp & 15) || d->kp % 8) return 1;
   if (d->out_ps % 4 || d->out_c0 % 4 || ((uintptr_t)d->out & 7)) return 1;
   if ((d->flags & RDN_EPI_STORE_PRE) && (d->pre_ps % 4 || ((uintptr_t)d->pre & 7))) return 1;

@@ -346,11 +346,7 @@ int launch_h(const rdn_conv_desc* d, hipStream_t st) {
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
   }
-  static const bool no_pair = [] {
-    const char* e = getenv("RDN_HALO_PAIR");
-    return e && e[0] == '0';
-  }();
-  const bool pair = !no_pair && blocks <= 2 * (int64_t)cus;
+  const bool pair = blocks <= 2 * (int64_t)cus;
   RDN_PROBE("conv3_halo_kernel<%s,%d,%d,%d%s%s>", rdn_tname<T>(), BN, WMW, CK, d->gate ? ",gate" : "",
             pair && sizeof(T) == 2 && BN <= 96 ? ",pair" : "");
   if (d->gate) {
@@ -386,18 +382,12 @@ static int pick_bn_cols(int ncols) {
 // minimum grid before BN is halved: a 32x32 level-3 layer has only 128 pixel tiles
 // per 16 images, so BN=128 would leave half of the 256 CUs idle (A/B on MI355X,
 // whole train step: 128 blocks 1351, 256 blocks 1338, 512 blocks 1369 img/s)
-static int min_blocks() {
-  static const int v = [] {
-    const char* e = getenv("RDN_MIN_BLOCKS");
-    return e ? atoi(e) : 512;
-  }();
-  return v;
-}
+constexpr int MIN_BLOCKS = 512;
 
 static int pick_bn(int ncols, int64_t tiles) {
   int bn = pick_bn_cols(ncols);
   while ((bn == 128 || bn == 64) && ncols % (bn / 2) == 0 &&
-         tiles * ((ncols + bn - 1) / bn) < (int64_t)min_blocks())
+         tiles * ((ncols + bn - 1) / bn) < (int64_t)MIN_BLOCKS)
     bn /= 2;
   return bn;
 }

@@ -64,7 +64,7 @@ struct WsCfg {
   static constexpr int BLK_PER_CU = LDS <= LDS_2BLK ? 2 : 1;
 };
 
-template <int BN, int CK, bool GATE, int DEPTH>
+template <int BN, int CK, bool GATE>
 __global__ __launch_bounds__(NT, 2) void conv3_ws_kernel(rdn_conv_desc d, int tiles_x, int tiles_y, int ntiles) {
   using Cfg = WsCfg<BN, CK>;
   constexpr int VEC = 8;
@@ -199,11 +199,10 @@ __global__ __launch_bounds__(NT, 2) void conv3_ws_kernel(rdn_conv_desc d, int ti
     for (int q = 0; q < VEC; ++q) galpha[q] = d.gate_alpha[(tid % HU) * VEC + q];
   }
 
-  // halo tiles in flight: DEPTH 2 keeps two tiles' global loads outstanding (register
-  // sets A/B) while one tile computes; each block otherwise waits a full HBM round
-  // trip per tile (the L0 layers are latency-bound at one tile in flight)
+  // one tile's halo loads in flight in registers while the tile in LDS computes (a
+  // second tile in flight, r02, cost occupancy and made the level-0 layers 0-20 % slower)
   constexpr int GH = GATE ? H_IT : 1;
-  u32x4 hA[H_IT], gA[GH], hB[H_IT], gB[GH];
+  u32x4 hA[H_IT], gA[GH];
   auto origin = [&](int tt, int& oy, int& ox, int& on) {
     const int tx = tt % tiles_x;
     tt /= tiles_x;
@@ -378,34 +377,20 @@ __global__ __launch_bounds__(NT, 2) void conv3_ws_kernel(rdn_conv_desc d, int ti
   load_epi(y0, x0, nimg);
   store_halo(hA, gA);
   __syncthreads();
-  // invariant at a step: LDS holds tile t; the next tile's loads (t1) are in flight
-  // in one register set (DEPTH 2) and the tile after (t2) is issued into the other
-  int t1 = t + per, y1 = 0, x1 = 0, n1 = 0;
-  origin(min(t1, t_last), y1, x1, n1);
-  if constexpr (DEPTH == 2) load_halo(y1, x1, n1, hA, gA);
-  auto step = [&](u32x4 (&hn)[H_IT], u32x4 (&gn)[GH], u32x4 (&hf)[H_IT], u32x4 (&gf)[GH]) -> bool {
-    // hn/gn: the next tile's registers; hf/gf: free for the tile after it
-    int y2 = 0, x2 = 0, n2 = 0;
-    const int t2 = t1 + per;
-    origin(min(t2, t_last), y2, x2, n2);
-    if constexpr (DEPTH == 2) {
-      load_halo(y2, x2, n2, hf, gf);   // in flight during the next TWO tiles
-    } else {
-      load_halo(y1, x1, n1, hn, gn);   // in flight during this tile's MFMAs and epilogue
-    }
+  // invariant at a step: LDS holds tile t; the next tile's (t1) loads are issued into
+  // the registers before its MFMAs and stored to LDS after its epilogue
+  int t1 = t + per;
+  for (;;) {
+    int y1 = 0, x1 = 0, n1 = 0;
+    origin(min(t1, t_last), y1, x1, n1);
+    load_halo(y1, x1, n1, hA, gA);   // in flight during this tile's MFMAs and epilogue
     compute_tile(y0, x0, nimg);
-    if (t1 >= t_hi) return false;
-    load_epi(y1, x1, n1);   // in flight during the next tile's MFMAs
-    store_halo(hn, gn);
+    if (t1 >= t_hi) break;
+    load_epi(y1, x1, n1);            // in flight during the next tile's MFMAs
+    store_halo(hA, gA);
     __syncthreads();
-    t = t1; y0 = y1; x0 = x1; nimg = n1;
-    t1 = t2; y1 = y2; x1 = x2; n1 = n2;
-    return true;
-  };
-  if constexpr (DEPTH == 2) {
-    while (step(hA, gA, hB, gB) && step(hB, gB, hA, gA)) {}
-  } else {
-    while (step(hA, gA, hB, gB)) {}
+    y0 = y1; x0 = x1; nimg = n1;
+    t1 += per;
   }
 }
 
@@ -427,34 +412,16 @@ int resident_per_cu(K kernel, int cap) {
   return n < cap ? n : cap;
 }
 
-template <int BN, int CK, bool GATE, int DEPTH>
+template <int BN, int CK, bool GATE>
 int launch_ws_k(const rdn_conv_desc* d, hipStream_t st, int tiles_x, int tiles_y, int ntiles, int cus) {
-  auto kern = conv3_ws_kernel<BN, CK, GATE, DEPTH>;
-  // RDN_WS_BPC: persistent blocks per CU (experiments); default = what is resident
-  static const int bpc_env = [] {
-    const char* e = getenv("RDN_WS_BPC");
-    return e ? atoi(e) : 0;
-  }();
-  static const int bpc = bpc_env > 0 ? bpc_env : resident_per_cu(kern, 4);
+  auto kern = conv3_ws_kernel<BN, CK, GATE>;
+  static const int bpc = resident_per_cu(kern, 4);   // persistent blocks per CU: what is resident
   const int per_xcd = (ntiles + 7) / 8;
   int slots = cus * bpc / 8;
   if (slots > per_xcd) slots = per_xcd;
   if (slots < 1) slots = 1;
   hipLaunchKernelGGL(kern, dim3((unsigned)(8 * slots)), dim3(NT), 0, st, *d, tiles_x, tiles_y, ntiles);
   return rdn_check_launch("rdn_conv_fwd(conv3 ws)");
-}
-
-// halo tiles in flight per block: 2 when that instantiation compiled without
-// register spills (the second register set fits), else 1; RDN_WS_DEPTH=1|2 forces
-// one (experiments)
-template <int BN, int CK, bool GATE>
-int ws_depth() {
-  static const int depth = [] {
-    hipFuncAttributes a;
-    if (hipFuncGetAttributes(&a, (const void*)conv3_ws_kernel<BN, CK, GATE, 2>) != hipSuccess) return 1;
-    return a.localSizeBytes == 0 ? 2 : 1;
-  }();
-  return depth;
 }
 
 template <int BN, int CK>
@@ -485,34 +452,17 @@ int launch_ws(const rdn_conv_desc* d, hipStream_t st) {
       cached_cus = cus;
     }
     cus = cached_cus;
-    static const int depth_env = [] {
-      const char* e = getenv("RDN_WS_DEPTH");
-      return e ? atoi(e) : 0;
-    }();
     constexpr int HU = CK / 8;
     if (d->gate && NT % HU != 0) return 1;
-    // default 1: measured on the train step, the second tile in flight (and the
-    // registers it takes from occupancy) made the level-0 layers 0-20 % slower;
-    // RDN_WS_DEPTH=0 picks 2 wherever it compiles without spills
-    int depth = depth_env == 1 || depth_env == 2 ? depth_env : 1;
-    if (depth_env == 0 && getenv("RDN_WS_DEPTH")) {
-      if (d->gate) {
-        if constexpr (NT % HU == 0) depth = ws_depth<BN, CK, true>();
-      } else {
-        depth = ws_depth<BN, CK, false>();
-      }
-    }
-    RDN_PROBE("conv3_ws_kernel<bf16,%d,%d%s%s>", BN, CK, d->gate ? ",gate" : "", depth == 2 ? ",d2" : "");
+    RDN_PROBE("conv3_ws_kernel<bf16,%d,%d%s>", BN, CK, d->gate ? ",gate" : "");
     if (d->gate) {
       if constexpr (NT % HU == 0) {
-        return depth == 2 ? launch_ws_k<BN, CK, true, 2>(d, st, tiles_x, tiles_y, ntiles, cus)
-                          : launch_ws_k<BN, CK, true, 1>(d, st, tiles_x, tiles_y, ntiles, cus);
+        return launch_ws_k<BN, CK, true>(d, st, tiles_x, tiles_y, ntiles, cus);
       } else {
         return 1;
       }
     }
-    return depth == 2 ? launch_ws_k<BN, CK, false, 2>(d, st, tiles_x, tiles_y, ntiles, cus)
-                      : launch_ws_k<BN, CK, false, 1>(d, st, tiles_x, tiles_y, ntiles, cus);
+    return launch_ws_k<BN, CK, false>(d, st, tiles_x, tiles_y, ntiles, cus);
   }
 }
 

@@ -435,14 +435,9 @@ int rdn_conv3_wsd_launch(const rdn_conv_desc* d, int ck, hipStream_t st) {
   // convs with 96-channel inputs (level-1 conv_1 46 -> 32 us, up_0 123 -> 112 us)
   // and the 64 -> 32 level-1 forward; elsewhere conv3_ws's 2-3 resident blocks per
   // CU hide more latency, and the gated input gradients (80 columns: 138 -> 128 us
-  // alone) lost it again beside the weight-gradient stream (RDN_CONV3_WSD=all takes
-  // this path for every full-tile shape)
-  static const bool all = [] {
-    const char* e = getenv("RDN_CONV3_WSD");
-    return e && e[0] == 'a';
-  }();
+  // alone) lost it again beside the weight-gradient stream
   const int bn16 = (d->ncols + 15) / 16 * 16;
-  if (!all && (d->gate || !(ck == 96 || (bn16 == 32 && ck == 64)))) return 1;
+  if (d->gate || !(ck == 96 || (bn16 == 32 && ck == 64))) return 1;
   if (d->h % TH || d->w % TW) return 1;                          // full tiles only
   const int flags = d->flags;
   if (flags & (RDN_EPI_OUT_NCHW | RDN_EPI_SCATTER2)) return 1;

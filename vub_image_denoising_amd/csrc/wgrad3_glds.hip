@@ -18,10 +18,10 @@
 // retires the reads of the stage the next DMA overwrites (it was read one tile
 // earlier).
 //
-// GATE (the level-0/1 single-chunk layers): the saved PReLU input arrives by DMA
-// beside dY and one pass over the LDS tile turns dY into dYpre in place (aten's
-// PReLU backward), accumulating the dalpha / dbias partials of the block's
-// channels in registers; they are written per split like rdn_prelu_bwd's.
+// Multi-chunk (level-1..3) launches only: the single-chunk level-0/1 weight
+// gradients, where the PReLU backward is fused into the loader, stay on the rows
+// kernel (a gated variant of this one was faster alone but its one 135-KB block per
+// CU on the weight-gradient stream cost the dgrad chain more: 1490 vs 1497 img/s, r02).
 //
 // LDS images.  One DMA wave-instruction writes 1 KiB contiguously (lane l ->
 // bytes l*16..l*16+15), so the images are dense rows (dY: BM*2 bytes per pixel;
@@ -38,7 +38,7 @@
 // reach the MFMAs.
 #include "rdn_common.h"
 
-#include <cstdlib>
+
 #include <type_traits>
 
 namespace {
@@ -49,7 +49,7 @@ constexpr int TH = 8, TW = 16, TP = TH * TW;
 constexpr int HW_ = TW + 2, HP = (TH + 2) * HW_;
 constexpr int LDS_MAX = 160 * 1024;
 
-template <int BM, int CK, bool GATE>
+template <int BM, int CK>
 struct Geo {
   static constexpr int NW = 4, NTH = 256;                // waves per block (one per SIMD)
   static constexpr int NCOL = 9 * CK, NT_ALL = (NCOL + 15) / 16;
@@ -62,10 +62,10 @@ struct Geo {
   static constexpr int RA = BM * 2, RB = CK * 2;          // bytes per dY / halo pixel row
   static constexpr int UA = RA / 16, UB = RB / 16;        // 16-B units per row
   static constexpr int A_PIECES = TP * RA / 1024;
-  static constexpr int PA = A_PIECES / NW;                // dY (and PReLU-input) pieces per wave and tile
+  static constexpr int PA = A_PIECES / NW;                // dY pieces per wave and tile
   static constexpr int HPC = (HP * RB + 1023) / 1024;     // halo pieces (wave w: w, w+4, ...)
   static constexpr int HPW = (HPC + NW - 1) / NW;
-  static constexpr int B_OFF = (GATE ? 2 : 1) * A_PIECES * 1024;
+  static constexpr int B_OFF = A_PIECES * 1024;
   static constexpr int STAGE = B_OFF + HPC * 1024;
   static constexpr int NS = 3 * STAGE <= LDS_MAX ? 3 : 2;
   static constexpr bool OK = NS * STAGE <= LDS_MAX && MTW >= 1;
@@ -86,9 +86,8 @@ __device__ __forceinline__ int rot(int x) {
 
 template <int N>
 __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
-__device__ __forceinline__ void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-// DMAs wave w issues per tile: PA_ dY (+ PReLU-input) pieces + halo pieces w, w+4, ... < HPC
+// DMAs wave w issues per tile: PA_ dY pieces + halo pieces w, w+4, ... < HPC
 template <int PA_, int HPC>
 __device__ __forceinline__ void wait_own(int wave, bool one_ahead) {
   if (!one_ahead) { wait_vm<0>(); return; }
@@ -117,10 +116,10 @@ __device__ __forceinline__ unsigned lds_addr(const unsigned char* p) {
   return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) unsigned char*)p;
 }
 
-template <int BM, int CK, bool GATE>
+template <int BM, int CK>
 __global__ __launch_bounds__(256, 1) void wgrad3_glds_kernel(rdn_wgrad_desc d, int tiles_x, int tiles_y, int ntiles,
                                                              int tiles_per_block) {
-  using G_ = Geo<BM, CK, GATE>;
+  using G_ = Geo<BM, CK>;
   constexpr int RA = G_::RA, RB = G_::RB, UA = G_::UA, UB = G_::UB, NW = G_::NW, MTW = G_::MTW, NTW = G_::NTW;
   constexpr int NS = G_::NS, PA = G_::PA, HPC = G_::HPC, HPW = G_::HPW;
   constexpr int VEC = 8;
@@ -137,12 +136,11 @@ __global__ __launch_bounds__(256, 1) void wgrad3_glds_kernel(rdn_wgrad_desc d, i
   const int t_cnt = max(0, min(t_beg + tiles_per_block, ntiles) - t_beg);
   const int H = d.h, W = d.w;
   const bf16* __restrict__ A = (const bf16*)d.a;
-  const bf16* __restrict__ Gt = (const bf16*)d.a_gate;
   const bf16* __restrict__ Bx = (const bf16*)d.b;
   const bf16* const zero = (const bf16*)g_wglds_zero;
 
   // ---- per-lane DMA source geometry (tile-invariant)
-  int a_rel[PA], g_rel[GATE ? PA : 1], a_py[PA], a_px[PA];
+  int a_rel[PA], a_py[PA], a_px[PA];
   bool a_ok[PA];
 #pragma unroll
   for (int j = 0; j < PA; ++j) {
@@ -154,8 +152,6 @@ __global__ __launch_bounds__(256, 1) void wgrad3_glds_kernel(rdn_wgrad_desc d, i
     a_py[j] = r / TW;
     a_px[j] = px;
     a_rel[j] = (a_py[j] * W + px) * (int)d.a_ps + rdn_coff32(d.a_c0 + (a_ok[j] ? m : 0), (int)d.a_ps, (int)d.a_pl);
-    if constexpr (GATE)
-      g_rel[j] = (a_py[j] * W + px) * (int)d.a_gate_ps + rdn_coff32(a_ok[j] ? m : 0, (int)d.a_gate_ps, (int)d.a_gate_pl);
   }
   int b_rel[HPW], b_hy[HPW], b_hx[HPW];
   bool b_ok[HPW];
@@ -178,15 +174,12 @@ __global__ __launch_bounds__(256, 1) void wgrad3_glds_kernel(rdn_wgrad_desc d, i
     const bool full = y0 + TH <= H && x0 + TW <= W;
     const bool interior = y0 >= 1 && y0 + TH + 1 <= H && x0 >= 1 && x0 + TW + 1 <= W;
     const bf16* const ab = A + pix0 * d.a_ps;
-    const bf16* const gb = GATE ? Gt + pix0 * d.a_gate_ps : nullptr;
     const bf16* const hb = Bx + (pix0 - W - 1) * d.b_ps;   // halo pixel (0, 0) = image (y0 - 1, x0 - 1)
     const unsigned st = lds_addr(lds) + stage * G_::STAGE;
 #pragma unroll
     for (int j = 0; j < PA; ++j) {
       const bool ok = a_ok[j] & (full | ((y0 + a_py[j] < H) & (x0 + a_px[j] < W)));
       glds16(ok ? (const void*)(ab + a_rel[j]) : (const void*)zero, st + (wave + NW * j) * 1024);
-      if constexpr (GATE)
-        glds16(ok ? (const void*)(gb + g_rel[j]) : (const void*)zero, st + (G_::A_PIECES + wave + NW * j) * 1024);
     }
 #pragma unroll
     for (int j = 0; j < HPW; ++j) {
@@ -194,40 +187,6 @@ __global__ __launch_bounds__(256, 1) void wgrad3_glds_kernel(rdn_wgrad_desc d, i
       const bool ok = b_ok[j] & (interior | (((unsigned)(y0 - 1 + b_hy[j]) < (unsigned)H) &
                                              ((unsigned)(x0 - 1 + b_hx[j]) < (unsigned)W)));
       glds16(ok ? (const void*)(hb + b_rel[j]) : (const void*)zero, st + G_::B_OFF + (wave + NW * j) * 1024);
-    }
-  };
-
-  // ---- PReLU-backward gate (GATE): thread = one logical 16-B channel unit of
-  // pixel rows tid/UA, tid/UA + 256/UA, ...; its 8 channels are fixed for the launch
-  constexpr int GROWS = 256 / UA;                          // rows per pass
-  const int gu = tid % UA;
-  float galpha[GATE ? VEC : 1], sa[GATE ? VEC : 1], sb[GATE ? VEC : 1];
-  const bool do_part = GATE && d.part != nullptr && by == 0;
-  if constexpr (GATE) {
-#pragma unroll
-    for (int k = 0; k < VEC; ++k) {
-      const int m = m0 + gu * VEC + k;
-      galpha[k] = m < d.mdim ? d.a_gate_alpha[m] : 0.f;
-      sa[k] = 0.f;
-      sb[k] = 0.f;
-    }
-  }
-  auto gate_pass = [&](int stage) {
-    unsigned char* const st = lds + stage * G_::STAGE;
-#pragma unroll
-    for (int pr = tid / UA; pr < TP; pr += GROWS) {
-      const int off = pr * RA + ((gu + rot<RA>(pr % TW)) % UA) * 16;
-      float dy[VEC], x[VEC];
-      Unit16<bf16>::unpack(*(const u32x4*)(st + off), dy);
-      Unit16<bf16>::unpack(*(const u32x4*)(st + G_::A_PIECES * 1024 + off), x);
-#pragma unroll
-      for (int k = 0; k < VEC; ++k) {
-        const bool pos = x[k] > 0.f;
-        if (!pos) sa[k] += x[k] * dy[k];
-        dy[k] = pos ? dy[k] : galpha[k] * dy[k];
-        sb[k] += dy[k];   // dbias sums dYpre before its rounding, as rdn_prelu_bwd does
-      }
-      *(u32x4*)(st + off) = Unit16<bf16>::pack(dy);
     }
   };
 
@@ -291,22 +250,15 @@ __global__ __launch_bounds__(256, 1) void wgrad3_glds_kernel(rdn_wgrad_desc d, i
 
   // ---- NS-deep ring: up to NS-1 tiles in flight while tile it is multiplied;
   // unrolled by NS so that every stage offset is a constant
-  constexpr int PA_ALL = PA * (GATE ? 2 : 1);
   for (int k = 0; k < NS - 1; ++k)
     if (k < t_cnt) issue(t_beg + k, k);
   auto step = [&](int it, auto S) {
     constexpr int s = decltype(S)::value;
     // own DMAs of tile it landed (with NS = 3 tile it+1 may still fly)
-    wait_own<PA_ALL, HPC>(wave, NS == 3 && it + 1 < t_cnt);
+    wait_own<PA, HPC>(wave, NS == 3 && it + 1 < t_cnt);
     __builtin_amdgcn_s_barrier();           // everyone's landed; everyone done reading tile it-1's stage
     asm volatile("" ::: "memory");
     if (it + NS - 1 < t_cnt) issue(t_beg + it + NS - 1, (s + NS - 1) % NS);
-    if constexpr (GATE) {
-      gate_pass(s);
-      wait_lgkm0();
-      __builtin_amdgcn_s_barrier();         // gated dY visible to every wave
-      asm volatile("" ::: "memory");
-    }
     compute(s);
   };
   for (int it = 0; it < t_cnt; it += NS) {
@@ -314,34 +266,6 @@ __global__ __launch_bounds__(256, 1) void wgrad3_glds_kernel(rdn_wgrad_desc d, i
     if (it + 1 < t_cnt) step(it + 1, std::integral_constant<int, 1 % NS>{});
     if constexpr (NS == 3)
       if (it + 2 < t_cnt) step(it + 2, std::integral_constant<int, 2 % NS>{});
-  }
-
-  if constexpr (GATE) {
-    if (do_part) {
-      // per-block channel partials -> part[split][0|1][m] (LDS reduce, fixed order)
-      wait_vm<0>();
-      __syncthreads();   // every wave done with the ring
-      float* red = (float*)lds;
-#pragma unroll
-      for (int k = 0; k < VEC; ++k) {
-        red[tid * VEC + k] = sa[k];
-        red[256 * VEC + tid * VEC + k] = sb[k];
-      }
-      __syncthreads();
-      if (tid < BM) {
-        const int cg = tid / VEC, k = tid % VEC;
-        float a = 0.f, b = 0.f;
-        for (int r = 0; r < GROWS; ++r) {
-          a += red[(r * UA + cg) * VEC + k];
-          b += red[256 * VEC + (r * UA + cg) * VEC + k];
-        }
-        const int m = m0 + tid;
-        if (m < d.mdim) {
-          d.part[((int64_t)bz * 2 + 0) * d.mdim + m] = a;
-          d.part[((int64_t)bz * 2 + 1) * d.mdim + m] = b;
-        }
-      }
-    }
   }
 
   // D[m][n]: row = g*4 + e (output channel), col = li (tile column)
@@ -366,16 +290,10 @@ __global__ __launch_bounds__(256, 1) void wgrad3_glds_kernel(rdn_wgrad_desc d, i
 
 template <int BM, int CK>
 int launch(const rdn_wgrad_desc* d, int blocks, int tiles_x, int tiles_y, int ntiles, int tpb, hipStream_t st) {
-  if (d->a_gate) {
-    if constexpr (Geo<BM, CK, true>::OK) {
-      RDN_PROBE("wgrad3_glds_kernel<bf16,%d,%d,gate>", BM, CK);
-      wgrad3_glds_kernel<BM, CK, true><<<blocks, 256, 0, st>>>(*d, tiles_x, tiles_y, ntiles, tpb);
-      return rdn_check_launch("rdn_conv_wgrad(conv3 glds)");
-    }
-  } else {
-    if constexpr (Geo<BM, CK, false>::OK) {
+  if constexpr (Geo<BM, CK>::OK) {
+    if (!d->a_gate) {
       RDN_PROBE("wgrad3_glds_kernel<bf16,%d,%d>", BM, CK);
-      wgrad3_glds_kernel<BM, CK, false><<<blocks, 256, 0, st>>>(*d, tiles_x, tiles_y, ntiles, tpb);
+      wgrad3_glds_kernel<BM, CK><<<blocks, 256, 0, st>>>(*d, tiles_x, tiles_y, ntiles, tpb);
       return rdn_check_launch("rdn_conv_wgrad(conv3 glds)");
     }
   }
@@ -405,27 +323,17 @@ int launch_ck(const rdn_wgrad_desc* d, int ck, int blocks, int tiles_x, int tile
 // channel group (the level-0/1 layers, where the PReLU gate is fused); else the
 // multi-chunk (level-1..3) launches.
 int rdn_wgrad3_glds_pick(const rdn_wgrad_desc* d, int single_chunk, int* bm, int* ck) {
-  // RDN_WGLDS: unset = multi-chunk launches only; "0" = never; "l0" = also the
-  // single-chunk level-0/1 ones.  Measured on the train step (r02, same box,
-  // interleaved): the single-chunk kernels are faster alone (32 x 80 gated: 140 ->
-  // 96 us) but one 135-KB-LDS block per CU on the weight-gradient stream keeps the
-  // dgrad chain's blocks off those CUs: 1490 vs 1497 img/s, so they stay opt-in
-  static const char* env = getenv("RDN_WGLDS");
-  const bool off = env && env[0] == '0';
-  const bool no_l0 = !(env && env[0] == 'l');
-  if (off || d->dtype != RDN_BF16) return 0;
-  if (single_chunk) {
-    // 32-row blocks only: the 16-row level-0 layers were equal or slower alone (one
-    // resident block per CU against the rows kernel's two)
-    if (no_l0 || d->mdim <= 16 || d->mdim > 64 || d->ndim > 96 || d->ndim % 16) return 0;
-    *bm = d->mdim <= 16 ? 16 : d->mdim <= 32 ? 32 : 64;
-    *ck = d->ndim;
-    // 64-row blocks only up to 64 channels (the gated 64 x 80 spills, 64 x 96 does not fit)
-    return *bm < 64 || *ck <= 64;
-  }
-  if (d->mdim < 32 || d->ndim % 32) return 0;   // (gated here only with RDN_FUSE_MAX_CHUNKS > 1)
+  if (single_chunk || d->dtype != RDN_BF16 || d->a_gate) return 0;
+  if (d->mdim < 32 || d->ndim % 32) return 0;
   *bm = d->mdim <= 32 ? 32 : 64;
   *ck = d->ndim % 64 == 0 ? 64 : 32;
+  // the narrow level-1 layers (96 / 128 / 160 input channels): whole-row or half-row
+  // channel groups, so operand A (dYpre) is read 1-2 times instead of 2-5 (per-layer
+  // A/B, r03_v6: level-1 conv_1 / conv_3 weight gradients -10..-20 %, up_0 -28 %)
+  if (d->ndim <= 160) {
+    if (d->ndim % 96 == 0) *ck = 96;
+    else if (d->ndim % 80 == 0) *ck = 80;   // (128 as one group: 43 -> 45 us, kept at 2 x 64)
+  }
   return 1;
 }
 

@@ -577,13 +577,10 @@ Plan plan(const rdn_wgrad_desc* d) {
     p.mtiles = (d->mdim + p.bm - 1) / p.bm;
     p.chunks = d->ndim / p.ck;
     const int base = p.mtiles * p.chunks;
-    // blocks per launch (RDN_WGLDS_BLOCKS): 192 of the 256 CUs, leaving room beside
-    // the dgrad chain; step A/B (3 interleaved rounds, same box): 128: 1483, 192:
-    // 1506, 256: 1499, 512: 1416 img/s (past 256 the 1-per-CU blocks run in two waves)
-    static const int gtarget = [] {
-      const char* e = getenv("RDN_WGLDS_BLOCKS");
-      return e && atoi(e) > 0 ? atoi(e) : 192;
-    }();
+    // blocks per launch: 192 of the 256 CUs, leaving room beside the dgrad chain;
+    // step A/B (3 interleaved rounds, same box): 128: 1483, 192: 1506, 256: 1499,
+    // 512: 1416 img/s (past 256 the 1-per-CU blocks run in two waves)
+    constexpr int gtarget = 192;
     int s = d->splits > 0 ? d->splits : gtarget / base;
     const int maxs = (p.ntiles + 1) / 2;                             // >= 2 tiles per block
     if (s > maxs) s = maxs;
@@ -595,14 +592,11 @@ Plan plan(const rdn_wgrad_desc* d) {
   p.mtiles = (d->mdim + p.bm - 1) / p.bm;
   p.chunks = d->ndim / p.ck;
   const int base = p.mtiles * p.chunks;
-  // blocks per launch (RDN_WGRAD_BLOCKS): one per CU.  The weight gradients run on
-  // the side stream beside the dgrad chain, where fewer, longer blocks (and half
-  // the split-K slab bytes) won: whole step 1342 (512) -> 1362 (256) img/s; 128:
-  // 1165, 192: 1302, 384: 1355, 1024: 1311
-  static const int target = [] {
-    const char* e = getenv("RDN_WGRAD_BLOCKS");
-    return e && atoi(e) > 0 ? atoi(e) : 256;
-  }();
+  // blocks per launch: one per CU.  The weight gradients run on the side stream
+  // beside the dgrad chain, where fewer, longer blocks (and half the split-K slab
+  // bytes) won: whole step 1342 (512) -> 1362 (256) img/s; 128: 1165, 192: 1302,
+  // 384: 1355, 1024: 1311
+  constexpr int target = 256;
   int s = d->splits > 0 ? d->splits : (target + base - 1) / base;
   const int maxs = (p.ntiles + 3) / 4;                             // >= 4 tiles per block
   if (s > maxs) s = maxs;

@@ -181,12 +181,13 @@ _FLAT_REGISTRY: list = []
 TRACER = None
 
 # PReLU backward is fused into a layer's dgrad/wgrad loaders when its weight-gradient
-# kernel reads the gated operand in at most this many input-channel chunks
-FUSE_MAX_CHUNKS = int(os.environ.get("RDN_FUSE_MAX_CHUNKS", "1"))
+# kernel reads the gated operand in ONE input-channel chunk (re-gating it per chunk
+# cost more than the separate pass it saves, r02 A/B)
+FUSE_PRELU = os.environ.get("RDN_FUSE_PRELU", "1") != "0"
 # weight gradients on a side stream (overlapped with the dgrad chain) and the depth
 # of the dYpre ring that decouples the two chains
 WGRAD_STREAM = os.environ.get("RDN_WGRAD_STREAM", "1") != "0"
-WGRAD_SLOTS = max(2, int(os.environ.get("RDN_WGRAD_SLOTS", "4")))
+WGRAD_SLOTS = 4
 # bench.py's per-kernel profiling pass serialises the backward (isolated kernel times)
 SERIAL_BWD = False
 # channel-blocked ("planar") activation buffers: a level-l buffer is [C/cb, P, cb] with
@@ -196,12 +197,6 @@ PLANAR = os.environ.get("RDN_PLANAR", "1") != "0"
 # gated level-0 convs: input + weight gradient in one fused kernel on the compute
 # stream (rdn_conv_dgrad_wgrad) instead of dgrad there and wgrad on the side stream
 FUSE_DW = os.environ.get("RDN_DW", "1") != "0"
-# where the fused layers' split-K reduce runs: "main" (default: right behind the fused
-# kernel; interleaved step A/B 1652 vs 1636 img/s -- at level 0 the side stream has
-# nothing else to overlap) or "side"
-DW_REDUCE = os.environ.get("RDN_DW_REDUCE", "main")
-# extra elements between two planes (keeps plane starts off power-of-two strides)
-PLANE_PAD = int(os.environ.get("RDN_PLANE_PAD", "0"))
 
 
 def find_flat(params):
@@ -555,7 +550,7 @@ class UNetEngine:
             cb = prog.cb.get(lvl, 0)
             if (PLANAR and cb and name not in in_bufs and name[1:] not in in_bufs and not name.startswith("PRE_")
                     and ch % cb == 0 and ch > cb):
-                pl = self.P[lvl] * cb + PLANE_PAD
+                pl = self.P[lvl] * cb
                 t = torch.zeros(ch // cb, pl, dtype=dtype, device=dev)
                 self.geo[name] = (cb, pl)
             else:
@@ -662,12 +657,12 @@ class UNetEngine:
             # PReLU backward inside their dgrad / wgrad loaders (gate = saved
             # PReLU input); the output conv (NCHW dy) and the 2x2 convs keep
             # the separate rdn_prelu_bwd pass producing dYpre.
-            fused = (L.kind == "c3" and L.ddst is not None) and os.environ.get("RDN_FUSE_PRELU", "1") != "0"
-            if fused:  # only when the wgrad re-reads operand A (with the gate) at most FUSE_MAX_CHUNKS times
+            fused = (L.kind == "c3" and L.ddst is not None) and FUSE_PRELU
+            if fused:  # only when the wgrad reads operand A (with the gate) in one chunk
                 n_, h_, w_ = self.grid[L.level]
                 probe = H.WgradDesc(dtype=self.code, gather=H.RDN_G_CONV3, n=n_, h=h_, w=w_, hin=h_, win=w_,
                                     mdim=L.cout, ndim=L.cin_pad)
-                fused = lib.rdn_wgrad_chunks(C.byref(probe)) <= FUSE_MAX_CHUNKS
+                fused = lib.rdn_wgrad_chunks(C.byref(probe)) == 1
             L.extra["fused"] = fused
             pre = self.bufs[L.pre]
             alpha = self.named[L.act + ".weight"]
@@ -968,8 +963,11 @@ class UNetEngine:
                         tr.stop(tok)
                     if rc:
                         H.check(rc, f"dgrad[{L.name}]")
-            rst = sst   # stream of this layer's reduce
-            if dw and DW_REDUCE == "main":
+            # stream of this layer's reduce: a fused layer's right behind its kernel on
+            # the main stream (interleaved step A/B 1652 vs 1636 img/s on the side
+            # stream -- at level 0 the side stream has nothing else to overlap)
+            rst = sst
+            if dw:
                 rst = st
             elif side is not None:
                 side.wait_event(L.extra["ev_ready"])
