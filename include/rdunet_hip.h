@@ -99,10 +99,27 @@ typedef struct rdn_conv_desc {
      out this way so conv_0..conv_2 do not drag the whole pixel row through HBM).
      Channel offsets (x_c0, ...) count across planes; ps % (16 B / elem) == 0. */
   int64_t x_pl, out_pl, pre_pl, res_pl, gate_pl;
+  /* optional PReLU backward fused into an INPUT-GRADIENT epilogue ("gate out",
+     RDN_G_CONV3 only): with gout != NULL the output columns [gout_c0, ncols) are
+     the complete gradient dY of the layer whose PReLU output is that input slice
+     (this conv is its last consumer in backward order, e.g. conv_k+1 for the
+     dense slice out_k, Unet_model.py:81-87).  Instead of storing dY there, the
+     epilogue writes that layer's dYpre (aten _prelu_kernel_backward):
+       gout[p][c'] = dY[p][c'] * (gout_pre[p][c'] > 0 ? 1 : gout_alpha[c']),
+       c' = c - gout_c0 (plain NHWC, strides gout_ps / gout_pre_ps),
+     and per-tile channel partials of its dalpha / conv-bias gradients
+       gout_part[row][0][c'] = sum_{pre<=0} pre*dY, gout_part[row][1][c'] = sum dYpre
+     over rdn_conv_gate_rows(d) rows (summed by rdn_wgrad_reduce, fixed order). */
+  void* gout; int64_t gout_ps; const void* gout_pre; int64_t gout_pre_ps;
+  const float* gout_alpha; float* gout_part; int32_t gout_c0;
 } rdn_conv_desc;
 
 /* Implicit-GEMM convolution (MFMA) with the fused epilogue above. */
 int rdn_conv_fwd(const rdn_conv_desc* d, void* stream);
+/* partial rows the gate-out epilogue of d writes (d->gout set; nothing is
+   launched); 0 when the kernel rdn_conv_fwd picks for d has no gate-out form
+   (launch the separate rdn_prelu_bwd instead) */
+int rdn_conv_gate_rows(const rdn_conv_desc* d);
 /* name of the kernel instantiation rdn_conv_fwd would launch for d (nothing is
    launched); for profiles and per-kernel timing */
 int rdn_conv_kernel_name(const rdn_conv_desc* d, char* buf, int32_t len);

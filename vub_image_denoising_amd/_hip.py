@@ -38,6 +38,8 @@ class ConvDesc(C.Structure):
         ("bm", _i32), ("bn", _i32),
         ("gate", _vp), ("gate_ps", _i64), ("gate_alpha", _vp),
         ("x_pl", _i64), ("out_pl", _i64), ("pre_pl", _i64), ("res_pl", _i64), ("gate_pl", _i64),
+        ("gout", _vp), ("gout_ps", _i64), ("gout_pre", _vp), ("gout_pre_ps", _i64),
+        ("gout_alpha", _vp), ("gout_part", _vp), ("gout_c0", _i32),
     ]
 
 
@@ -67,6 +69,7 @@ SIGNATURES = {
     "rdn_conv_fwd": (_i32, [C.POINTER(ConvDesc), _vp]),
     "rdn_conv_wgrad": (_i32, [C.POINTER(WgradDesc), _vp]),
     "rdn_conv_kernel_name": (_i32, [C.POINTER(ConvDesc), C.c_char_p, _i32]),
+    "rdn_conv_gate_rows": (_i32, [C.POINTER(ConvDesc)]),
     "rdn_wgrad_kernel_name": (_i32, [C.POINTER(WgradDesc), C.c_char_p, _i32]),
     "rdn_wgrad_splits": (_i32, [C.POINTER(WgradDesc)]),
     "rdn_conv_dgrad_wgrad": (_i32, [C.POINTER(ConvDesc), C.POINTER(WgradDesc), _vp]),

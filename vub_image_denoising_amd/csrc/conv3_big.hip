@@ -104,7 +104,7 @@ __device__ __forceinline__ void wait_split(int wave) {   // vmcnt(wave < SPLIT ?
   else wait_vm<NLO>();
 }
 
-template <int TH, int BN, int WM, int CK, int EP>
+template <int TH, int BN, int WM, int CK, int EP, bool GO>
 __global__ __launch_bounds__(NTB, 2) void conv3_big_kernel(rdn_conv_desc d, int tiles_x, int tiles_y, int nitems) {
   using Cfg = PtCfg<TH, BN, WM, CK>;
   constexpr int RB = Cfg::RB, RW = Cfg::RW, SPC = Cfg::SPC, SS = Cfg::SS;
@@ -112,6 +112,7 @@ __global__ __launch_bounds__(NTB, 2) void conv3_big_kernel(rdn_conv_desc d, int 
   constexpr bool FWD = EP == EP_FWD || EP == EP_FWD_RES;
   constexpr bool RES = EP == EP_FWD_RES || EP == EP_RES;
   constexpr bool ACC = EP == EP_ACC;
+  constexpr bool GOK = GO && !FWD;   // gate-out epilogue (input gradients only)
   static_assert(Cfg::OK, "conv3_big geometry");
 
   __shared__ __attribute__((aligned(1024))) unsigned char lds[Cfg::LDS];
@@ -137,6 +138,9 @@ __global__ __launch_bounds__(NTB, 2) void conv3_big_kernel(rdn_conv_desc d, int 
       tab[c] = d.bias[c];
       tab[COL_MAX + c] = d.alpha[c];
     }
+  }
+  if constexpr (GOK) {   // slopes of the gated layer (columns gout_c0.. of this conv)
+    for (int c = tid; c < d.ncols - d.gout_c0; c += NTB) tab[COL_MAX + c] = d.gout_alpha[c];
   }
 
   struct Geo { int nimg, y0, x0, n0; };
@@ -251,14 +255,19 @@ __global__ __launch_bounds__(NTB, 2) void conv3_big_kernel(rdn_conv_desc d, int 
   // (r, g) of fragment (i, jn) holds channels cl..cl+3 of tile pixel (row wm*MT + i,
   // column r): one 8-byte unit per operand.
   u32x2 eop[(RES || ACC) ? MT : 1][(RES || ACC) ? NTL : 1];
-  auto epilogue = [&](const Geo& q) {
+  u32x2 gpre[GOK ? MT : 1][GOK ? NTL : 1];
+  // epilogue operands (residual / accumulate target / gated layer's PReLU input),
+  // issued at the epilogue's start (issuing them at the start of the item's last K
+  // stage instead made the 80-column level-1 input gradient 67 -> 72 us: that
+  // stage's closing vmcnt(0) then waits on an HBM round trip)
+  auto epi_load = [&](const Geo& q) {
     const int64_t pix0 = ((int64_t)q.nimg * H + q.y0) * W + q.x0;
-    const __amdgpu_buffer_rsrc_t ro = rdn_rsrc((const bf16*)d.out + pix0 * d.out_ps);
-    const int ops = (int)d.out_ps, pps = (int)d.pre_ps;
     const bool col_ok = q.x0 + r < W;
-    if constexpr (RES || ACC) {   // operands first: their latency overlaps the loop below
+    if constexpr (RES || ACC) {
+      const int ops = (int)d.out_ps;
       const int eps = RES ? (int)d.res_ps : ops;
-      const __amdgpu_buffer_rsrc_t re = RES ? rdn_rsrc((const bf16*)d.res + pix0 * d.res_ps) : ro;
+      const __amdgpu_buffer_rsrc_t re =
+          rdn_rsrc(RES ? (const bf16*)d.res + pix0 * d.res_ps : (const bf16*)d.out + pix0 * d.out_ps);
 #pragma unroll
       for (int jn = 0; jn < NTL; ++jn) {
         const int cl = q.n0 + wn * WTN + jn * 16 + g * 4;
@@ -272,6 +281,26 @@ __global__ __launch_bounds__(NTB, 2) void conv3_big_kernel(rdn_conv_desc d, int 
         }
       }
     }
+    if constexpr (GOK) {   // saved PReLU input of the gated columns
+      const __amdgpu_buffer_rsrc_t rg = rdn_rsrc((const bf16*)d.gout_pre + pix0 * d.gout_pre_ps);
+      const int gps = (int)d.gout_pre_ps;
+#pragma unroll
+      for (int jn = 0; jn < NTL; ++jn) {
+        const int cl = q.n0 + wn * WTN + jn * 16 + g * 4;
+        const bool gok = col_ok & (cl >= d.gout_c0);
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+          gpre[i][jn] = rdn_ld8(rg, gok & (q.y0 + wm * MT + i < H), (((wm * MT + i) * W + r) * gps + cl - d.gout_c0) * 2);
+      }
+    }
+  };
+  auto epilogue = [&](const Geo& q, int itm) {
+    epi_load(q);
+    const int64_t pix0 = ((int64_t)q.nimg * H + q.y0) * W + q.x0;
+    const __amdgpu_buffer_rsrc_t ro = rdn_rsrc((const bf16*)d.out + pix0 * d.out_ps);
+    const __amdgpu_buffer_rsrc_t rgo = GOK ? rdn_rsrc((const bf16*)d.gout + pix0 * d.gout_ps) : ro;
+    const int ops = (int)d.out_ps, pps = (int)d.pre_ps;
+    const bool col_ok = q.x0 + r < W;
     const __amdgpu_buffer_rsrc_t rp = FWD ? rdn_rsrc((const bf16*)d.pre + pix0 * d.pre_ps) : ro;
 #pragma unroll
     for (int jn = 0; jn < NTL; ++jn) {
@@ -284,6 +313,7 @@ __global__ __launch_bounds__(NTB, 2) void conv3_big_kernel(rdn_conv_desc d, int 
       const int co = rdn_coff32(d.out_c0 + cl, ops, (int)d.out_pl);
       const int cp = FWD ? rdn_coff32(cl, pps, (int)d.pre_pl) : 0;
       const bool res_ok = RES ? cl < d.res_climit : true;
+      float gsa[4] = {0.f, 0.f, 0.f, 0.f}, gsb[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
         const bool ok = col_ok & (q.y0 + wm * MT + i < H);
@@ -304,9 +334,45 @@ __global__ __launch_bounds__(NTB, 2) void conv3_big_kernel(rdn_conv_desc d, int 
             v[2] += bf16lo(eop[i][jn][1]); v[3] += bf16hi(eop[i][jn][1]);
           }
         }
+        if constexpr (GOK) {
+          if (cl >= d.gout_c0) {   // complete dY of the gated layer: store its dYpre instead
+            const int gc = cl - d.gout_c0;
+            const f32x4 al = *(const f32x4*)(tab + COL_MAX + gc);
+            const float pr[4] = {bf16lo(gpre[i][jn][0]), bf16hi(gpre[i][jn][0]), bf16lo(gpre[i][jn][1]),
+                                 bf16hi(gpre[i][jn][1])};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const bool pos = pr[e] > 0.f;
+              if (ok && !pos) gsa[e] += pr[e] * v[e];
+              v[e] = pos ? v[e] : al[e] * v[e];
+              if (ok) gsb[e] += v[e];
+            }
+            int o = ok ? (prow * (int)d.gout_ps + gc) * 2 : RDN_OOB;
+            asm volatile("" : "+v"(o));
+            __builtin_amdgcn_raw_buffer_store_b64(rdn_pack4(v), rgo, o, 0, 0);
+            continue;
+          }
+        }
         int o = ok ? (prow * ops + co) * 2 : RDN_OOB;
         asm volatile("" : "+v"(o));
         __builtin_amdgcn_raw_buffer_store_b64(rdn_pack4(v), ro, o, 0, 0);
+      }
+      if constexpr (GOK) {
+        if (cl >= d.gout_c0) {   // this 16-lane group's channel partials over the item's pixels
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int m = 1; m < 16; m <<= 1) {
+              gsa[e] += __shfl_xor(gsa[e], m, 64);
+              gsb[e] += __shfl_xor(gsb[e], m, 64);
+            }
+          if (r == 0) {
+            const int gcn = d.ncols - d.gout_c0;
+            float* const prt = d.gout_part + ((int64_t)(itm / ncb) * WM + wm) * 2 * gcn + (cl - d.gout_c0);
+            *(f32x4*)prt = f32x4{gsa[0], gsa[1], gsa[2], gsa[3]};
+            *(f32x4*)(prt + gcn) = f32x4{gsb[0], gsb[1], gsb[2], gsb[3]};
+          }
+        }
       }
     }
   };
@@ -354,7 +420,7 @@ __global__ __launch_bounds__(NTB, 2) void conv3_big_kernel(rdn_conv_desc d, int 
       }
       hbuf ^= 1;
     }
-    epilogue(cur);   // global stores drain under the next item
+    epilogue(cur, item);   // global stores drain under the next item
     item = nxt_item;
     cur = nq;
   }
@@ -391,17 +457,18 @@ int epi_mode(const rdn_conv_desc* d) {
   return -1;
 }
 
-template <int TH, int BN, int WM, int CK, int EP>
+template <int TH, int BN, int WM, int CK, int EP, bool GO = false>
 int launch_pt(const rdn_conv_desc* d, hipStream_t st, int tiles_x, int tiles_y, int nitems) {
   if constexpr (!PtCfg<TH, BN, WM, CK>::OK) {
     return 1;
   } else {
-    RDN_PROBE("conv3_big_kernel<bf16,%d,%d,%d,%d>", TH, BN, WM, CK);
+    if (GO) rdn_probe_rows = (int)((int64_t)d->n * tiles_x * tiles_y * WM);
+    RDN_PROBE("conv3_big_kernel<bf16,%d,%d,%d,%d%s>", TH, BN, WM, CK, GO ? ",go" : "");
     const int per_xcd = (nitems + 7) / 8;
     int slots = cu_count() / 8;
     if (slots > per_xcd) slots = per_xcd;
     if (slots < 1) slots = 1;
-    hipLaunchKernelGGL((conv3_big_kernel<TH, BN, WM, CK, EP>), dim3((unsigned)(8 * slots)), dim3(NTB), 0, st, *d,
+    hipLaunchKernelGGL((conv3_big_kernel<TH, BN, WM, CK, EP, GO>), dim3((unsigned)(8 * slots)), dim3(NTB), 0, st, *d,
                        tiles_x, tiles_y, nitems);
     return rdn_check_launch("rdn_conv_fwd(conv3 big)");
   }
@@ -413,6 +480,14 @@ int launch_big(const rdn_conv_desc* d, hipStream_t st) {
   const int64_t nitems = (int64_t)d->n * tiles_x * tiles_y * (d->ncols / BN);
   if (nitems >= (1ll << 31)) return 1;
   const int ni = (int)nitems;
+  if (d->gout) {   // gate-out: the input-gradient modes only
+    switch (epi_mode(d)) {
+      case EP_PLAIN: return launch_pt<TH, BN, WM, CK, EP_PLAIN, true>(d, st, tiles_x, tiles_y, ni);
+      case EP_ACC: return launch_pt<TH, BN, WM, CK, EP_ACC, true>(d, st, tiles_x, tiles_y, ni);
+      case EP_RES: return launch_pt<TH, BN, WM, CK, EP_RES, true>(d, st, tiles_x, tiles_y, ni);
+    }
+    return 1;
+  }
   switch (epi_mode(d)) {
     case EP_FWD: return launch_pt<TH, BN, WM, CK, EP_FWD>(d, st, tiles_x, tiles_y, ni);
     case EP_FWD_RES: return launch_pt<TH, BN, WM, CK, EP_FWD_RES>(d, st, tiles_x, tiles_y, ni);
@@ -499,6 +574,10 @@ int rdn_conv3_big_launch(const rdn_conv_desc* d, int ck, hipStream_t st) {
   if (!fits(d->x_ps, d->x_pl, d->x_c0 + d->cin) || !fits(d->out_ps, d->out_pl, d->out_c0 + d->ncols) ||
       ((d->flags & RDN_EPI_STORE_PRE) && !fits(d->pre_ps, d->pre_pl, d->ncols)) ||
       ((d->flags & RDN_EPI_RESID) && !fits(d->res_ps, d->res_pl, d->res_c0 + d->res_climit)))
+    return 1;
+  if (d->gout && (d->ncols - d->gout_c0 > COL_MAX || d->gout_c0 % 4 || d->gout_ps % 4 || d->gout_pre_ps % 4 ||
+                  !fits(d->gout_ps, 0, d->ncols - d->gout_c0) || !fits(d->gout_pre_ps, 0, d->ncols - d->gout_c0) ||
+                  ((uintptr_t)d->gout_part & 15)))
     return 1;
   return ck == 64 ? big_dispatch<64>(d, st) : big_dispatch<32>(d, st);
 }

@@ -544,7 +544,7 @@ int dw_grid(int ntiles) {
 bool dw_serves(const rdn_conv_desc* d, const rdn_wgrad_desc* wg) {
   if (!dw_enabled() || !d || !wg) return false;
   if (d->dtype != RDN_BF16 || wg->dtype != RDN_BF16 || d->gather != RDN_G_CONV3 || wg->gather != RDN_G_CONV3) return false;
-  if (!d->gate || !wg->a_gate || !d->gate_alpha || d->bn || d->bm) return false;
+  if (!d->gate || !wg->a_gate || !d->gate_alpha || d->bn || d->bm || d->gout) return false;
   if (d->flags & ~(RDN_EPI_RESID | RDN_EPI_ACCUM)) return false;
   if ((d->flags & RDN_EPI_RESID) && (d->flags & RDN_EPI_ACCUM)) return false;
   if (d->h % TH || d->w % TW || d->n != wg->n || d->h != wg->h || d->w != wg->w) return false;

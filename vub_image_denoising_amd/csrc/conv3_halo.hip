@@ -63,7 +63,7 @@ __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_
   constexpr int MAIN_BYTES = HALO_BYTES + 2 * BN * RW;
   constexpr int CROW = BN * 4 + 16;                  // epilogue fp32 tile row
   constexpr int EPI_BYTES = BM * CROW;
-  constexpr int LDS_BYTES = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;
+  constexpr int LDS_BYTES = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;   // (>= the 4 x 2 x BN gate-out partials)
   constexpr bool KALIGN = CK % KSTEP == 0;           // a k-step never straddles a tap
   constexpr int UPR = BN / VEC, EU = BM * UPR, E_IT = (EU + NT - 1) / NT;
   constexpr bool COLFIX = NT % UPR == 0;             // a thread's output channels are fixed
@@ -258,6 +258,23 @@ __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_
   }
 
   // ---- epilogue: fp32 tile through LDS, then 16-byte NHWC units
+  const int flags = d.flags;
+  const bool fast = (d.ncols % VEC) == 0 && !(flags & RDN_EPI_OUT_NCHW) && y0 + TH <= H && x0 + TW <= W &&
+                    (!(flags & RDN_EPI_RESID) || (d.res_climit % VEC == 0 && d.res_ps % VEC == 0 &&
+                                                  d.res_c0 % VEC == 0)) &&
+                    d.out_ps % VEC == 0 && d.out_c0 % VEC == 0 && d.pre_ps % VEC == 0;
+  const int64_t opix0 = ((int64_t)nimg * H + y0) * W + x0;
+  // gate-out (d.gout): the columns [gout_c0, ncols) are a layer's complete dY --
+  // store its dYpre instead and sum the dalpha / dbias partials of the tile
+  // (the launcher takes gate-out only with COLFIX, full tiles and 16-B units)
+  const bool go = COLFIX && d.gout != nullptr;
+  float oalpha[VEC];   // slopes of the gated layer for this thread's channels (COLFIX)
+  const int ccol = n0 + (tid % UPR) * VEC;
+  {
+    const bool g_on = go && ccol >= d.gout_c0 && ccol < d.ncols;
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) oalpha[q] = g_on ? d.gout_alpha[ccol - d.gout_c0 + q] : 0.f;
+  }
   float* const Ct = (float*)lds;
 #pragma unroll
   for (int i = 0; i < MT; ++i)
@@ -268,20 +285,17 @@ __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_
         Ct[((wm * WTM + i * 16 + g * 4 + e) * CROW) / 4 + wn * WTN + jn * 16 + r] = acc[i][jn][e];
   __syncthreads();
 
-  const int flags = d.flags;
-  const bool fast = (d.ncols % VEC) == 0 && !(flags & RDN_EPI_OUT_NCHW) && y0 + TH <= H && x0 + TW <= W &&
-                    (!(flags & RDN_EPI_RESID) || (d.res_climit % VEC == 0 && d.res_ps % VEC == 0 &&
-                                                  d.res_c0 % VEC == 0)) &&
-                    d.out_ps % VEC == 0 && d.out_c0 % VEC == 0 && d.pre_ps % VEC == 0;
   if (!fast) {
     c3::store_tile<T, BN, NT>(d, Ct, CROW / 4, y0, x0, nimg, n0, tid);
     return;
   }
-  const int64_t opix0 = ((int64_t)nimg * H + y0) * W + x0;
+  float gsa[VEC], gsb[VEC];
+#pragma unroll
+  for (int q = 0; q < VEC; ++q) { gsa[q] = 0.f; gsb[q] = 0.f; }
   float ebias[VEC], ealpha[VEC];
   int64_t cf_pre = 0, cf_out = 0, cf_res = 0;
   if constexpr (COLFIX) {
-    const int c = n0 + (tid % UPR) * VEC;
+    const int c = ccol;
 #pragma unroll
     for (int q = 0; q < VEC; ++q) {
       ebias[q] = ((flags & RDN_EPI_BIAS) && c + q < d.ncols) ? d.bias[c + q] : 0.f;
@@ -331,7 +345,52 @@ __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_
 #pragma unroll
       for (int q = 0; q < VEC; ++q) v[q] += rv[q];
     }
+    if (go && c >= d.gout_c0) {   // dYpre = dY * (pre > 0 ? 1 : alpha); aten prelu backward
+      const int gc = c - d.gout_c0;
+      float pr[VEC];
+      Unit16<T>::unpack(*(const u32x4*)((const T*)d.gout_pre + opix * d.gout_pre_ps + gc), pr);
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) {
+        const bool pos = pr[q] > 0.f;
+        if (!pos) gsa[q] += pr[q] * v[q];
+        v[q] = pos ? v[q] : oalpha[q] * v[q];
+        gsb[q] += v[q];
+      }
+      *(u32x4*)((T*)d.gout + opix * d.gout_ps + gc) = Unit16<T>::pack(v);
+      continue;
+    }
     *(u32x4*)op = Unit16<T>::pack(v);
+  }
+  if (!go || n0 + BN <= d.gout_c0) return;
+  // per-channel partials of the tile: the lanes of a wave holding one channel group
+  // (lane, lane + UPR, ...) combine by xor shuffles, then the 4 waves through LDS,
+  // in a fixed order (the fp32 tile is consumed)
+  if constexpr (COLFIX) {
+#pragma unroll
+    for (int m = UPR; m < 64; m <<= 1)
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) {
+        gsa[q] += __shfl_xor(gsa[q], m, 64);
+        gsb[q] += __shfl_xor(gsb[q], m, 64);
+      }
+    __syncthreads();
+    float* const red = (float*)lds;   // [wave][2][BN]
+    if (lane < UPR) {
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) {
+        red[(wave * 2 + 0) * BN + lane * VEC + q] = gsa[q];
+        red[(wave * 2 + 1) * BN + lane * VEC + q] = gsb[q];
+      }
+    }
+    __syncthreads();
+    const int gcn = d.ncols - d.gout_c0;
+    float* const part = d.gout_part + (int64_t)(lb / ncb) * 2 * gcn;
+    for (int j = tid; j < 2 * BN; j += NT) {
+      const int which = j / BN, col = j - which * BN, c = n0 + col;
+      if (c < d.gout_c0 || c >= d.ncols) continue;
+      part[which * gcn + (c - d.gout_c0)] = (red[which * BN + col] + red[(2 + which) * BN + col]) +
+                                            (red[(4 + which) * BN + col] + red[(6 + which) * BN + col]);
+    }
   }
 }
 
@@ -347,6 +406,20 @@ int launch_h(const rdn_conv_desc* d, hipStream_t st) {
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
   }
   const bool pair = blocks <= 2 * (int64_t)cus;
+  if (d->gout) {
+    // gate-out only on the fast epilogue with a fixed channel group per thread
+    constexpr int VEC = TypeInfo<T>::VEC;
+    const bool colfix = NT % (BN / VEC) == 0 && BN % VEC == 0;
+    const bool full = d->h % TH == 0 && d->w % TW == 0 && d->ncols % VEC == 0 && !(d->flags & RDN_EPI_OUT_NCHW) &&
+                      d->out_ps % VEC == 0 && d->out_c0 % VEC == 0 &&
+                      (!(d->flags & RDN_EPI_RESID) || (d->res_climit % VEC == 0 && d->res_ps % VEC == 0 &&
+                                                       d->res_c0 % VEC == 0));
+    if (!colfix || !full) {
+      rdn_set_error("rdn_conv_fwd(conv3): gate-out needs full 8x16 tiles and a column tile of whole channel groups");
+      return RDN_E_SHAPE;
+    }
+    rdn_probe_rows = (int)(d->n * tiles_x * tiles_y);
+  }
   RDN_PROBE("conv3_halo_kernel<%s,%d,%d,%d%s%s>", rdn_tname<T>(), BN, WMW, CK, d->gate ? ",gate" : "",
             pair && sizeof(T) == 2 && BN <= 96 ? ",pair" : "");
   if (d->gate) {

@@ -486,7 +486,7 @@ int rdn_conv3_ws_launch(const rdn_conv_desc* d, int ck, hipStream_t st) {
 #ifdef RDN_NO_WS
   return 1;
 #endif
-  if (!ws_enabled() || d->dtype != RDN_BF16 || d->bn || ck != d->cin || d->ncols > 96) return 1;
+  if (!ws_enabled() || d->dtype != RDN_BF16 || d->bn || ck != d->cin || d->ncols > 96 || d->gout) return 1;
   if (d->x_ps % 8 || d->x_c0 % 8 || ((uintptr_t)d->x & 15) || ((uintptr_t)d->wp & 15) || d->kp % 8) return 1;
   switch (ck) {
     case 8: return ws_bn<8>(d, st);

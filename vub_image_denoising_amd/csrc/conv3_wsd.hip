@@ -430,7 +430,7 @@ int rdn_conv3_wsd_launch(const rdn_conv_desc* d, int ck, hipStream_t st) {
     const char* e = getenv("RDN_CONV3_WSD");
     return e && e[0] == '0';
   }();
-  if (off || d->dtype != RDN_BF16 || d->bn || ck != d->cin || d->ncols > 96 || d->ncols % 8) return 1;
+  if (off || d->dtype != RDN_BF16 || d->bn || ck != d->cin || d->ncols > 96 || d->ncols % 8 || d->gout) return 1;
   // where it beats conv3_ws (per-layer A/B on the train step, r02): the forward
   // convs with 96-channel inputs (level-1 conv_1 46 -> 32 us, up_0 123 -> 112 us)
   // and the 64 -> 32 level-1 forward; elsewhere conv3_ws's 2-3 resident blocks per

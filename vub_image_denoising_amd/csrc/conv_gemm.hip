@@ -359,6 +359,17 @@ extern "C" int rdn_conv_fwd(const rdn_conv_desc* d, void* stream) {
   if ((d->flags & RDN_EPI_RESID) && !((d->flags & RDN_EPI_OUT_NCHW) ? (const void*)d->res_nchw : d->res)) {
     rdn_set_error("rdn_conv_fwd: null residual"); return RDN_E_ARG;
   }
+  if (d->gout) {   // gate-out epilogue: an input gradient whose column tail is a layer's complete dY
+    if (d->gather != RDN_G_CONV3 || !d->gout_pre || !d->gout_alpha || !d->gout_part ||
+        (d->flags & ~(RDN_EPI_ACCUM | RDN_EPI_RESID)) || d->gout_c0 <= 0 || d->gout_c0 >= d->ncols ||
+        d->gout_c0 % vec || d->ncols % vec || d->gout_ps % vec || d->gout_pre_ps % vec ||
+        d->gout_ps < d->ncols - d->gout_c0 || d->gout_pre_ps < d->ncols - d->gout_c0 ||
+        ((uintptr_t)d->gout & 15) || ((uintptr_t)d->gout_pre & 15)) {
+      rdn_set_error("rdn_conv_fwd: gate-out needs a 3x3 input gradient (no bias/PReLU epilogue), 0 < gout_c0 < ncols, "
+                    "16-byte units and rows");
+      return RDN_E_ARG;
+    }
+  }
   hipStream_t st = (hipStream_t)stream;
   if (d->gather == RDN_G_CONV3) return rdn_conv3_launch(d, st);  // LDS-halo kernel (conv3_halo.hip)
   if (d->gate) { rdn_set_error("rdn_conv_fwd: the PReLU gate is supported for RDN_G_CONV3 only"); return RDN_E_ARG; }

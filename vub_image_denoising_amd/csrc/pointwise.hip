@@ -27,6 +27,7 @@ extern "C" const char* rdn_last_error(void) { return g_err; }
 
 thread_local char* rdn_probe_buf = nullptr;
 thread_local int rdn_probe_len = 0;
+thread_local int rdn_probe_rows = 0;
 int rdn_probe_name(const char* fmt, ...) {
   va_list ap;
   va_start(ap, fmt);
@@ -42,6 +43,16 @@ extern "C" int rdn_conv_kernel_name(const rdn_conv_desc* d, char* buf, int32_t l
   const int rc = rdn_conv_fwd(d, nullptr);
   rdn_probe_buf = nullptr;
   return rc;
+}
+extern "C" int rdn_conv_gate_rows(const rdn_conv_desc* d) {
+  if (!d || !d->gout) return 0;
+  char buf[128];
+  rdn_probe_buf = buf;
+  rdn_probe_len = (int)sizeof(buf);
+  rdn_probe_rows = 0;
+  const int rc = rdn_conv_fwd(d, nullptr);
+  rdn_probe_buf = nullptr;
+  return rc == RDN_OK ? rdn_probe_rows : 0;
 }
 extern "C" int rdn_wgrad_kernel_name(const rdn_wgrad_desc* d, char* buf, int32_t len) {
   if (!buf || len < 1) { rdn_set_error("rdn_wgrad_kernel_name: no buffer"); return RDN_E_ARG; }

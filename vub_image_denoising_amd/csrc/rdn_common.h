@@ -155,6 +155,8 @@ int rdn_check_launch(const char* what);
 // return without launching
 extern thread_local char* rdn_probe_buf;
 extern thread_local int rdn_probe_len;
+// rdn_conv_gate_rows: the launcher that would run sets the gate-out partial rows here
+extern thread_local int rdn_probe_rows;
 int rdn_probe_name(const char* fmt, ...);
 #define RDN_PROBE(...) \
   do {                 \

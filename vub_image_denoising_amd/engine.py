@@ -187,7 +187,9 @@ FUSE_PRELU = os.environ.get("RDN_FUSE_PRELU", "1") != "0"
 # weight gradients on a side stream (overlapped with the dgrad chain) and the depth
 # of the dYpre ring that decouples the two chains
 WGRAD_STREAM = os.environ.get("RDN_WGRAD_STREAM", "1") != "0"
-WGRAD_SLOTS = 4
+# (6 slots: 1690 / 1691 img/s against 1672 / 1673 with 4, 1681-1684 with 8, 1678-1682
+# with 12; interleaved on one box, profiles/r03_v9_slots_ab.txt)
+WGRAD_SLOTS = int(os.environ.get("RDN_WGRAD_SLOTS", "6"))
 # bench.py's per-kernel profiling pass serialises the backward (isolated kernel times)
 SERIAL_BWD = False
 # channel-blocked ("planar") activation buffers: a level-l buffer is [C/cb, P, cb] with
@@ -197,6 +199,15 @@ PLANAR = os.environ.get("RDN_PLANAR", "1") != "0"
 # gated level-0 convs: input + weight gradient in one fused kernel on the compute
 # stream (rdn_conv_dgrad_wgrad) instead of dgrad there and wgrad on the side stream
 FUSE_DW = os.environ.get("RDN_DW", "1") != "0"
+# PReLU backward of a layer fused into the input-gradient epilogue of its last
+# consumer in backward order (rdn_conv_desc.gout: conv_k+1 finishes dense slice
+# out_k, up_l.conv finishes up_l.conv_t's output), instead of a separate pass.
+# Off by default: per launch it saves 0.5-6 us at levels 2/3 (scripts/gate_kbench.py,
+# profiles/r03_v9_gate_kbench.json), but the whole step measured 1666-1674 img/s
+# with it against 1680-1691 without (8-16 vs 6-12 ring slots, interleaved,
+# profiles/r03_v9_slots_ab.txt): the longer finisher launches sit on the critical path
+# beside the weight-gradient stream.  Tested both ways (tests/test_gpu_gateout.py).
+GATE_OUT = os.environ.get("RDN_GATE_OUT", "0") == "1"
 
 
 def find_flat(params):
@@ -511,6 +522,10 @@ def weight_packs(module, fp, layers, dtype) -> WeightPacks:
 
 
 # ----------------------------------------------------------------- engine
+# descriptor pointers that select a kernel variant (kept as they are by the probes)
+_CONV_SELECT = ("gate", "gate_alpha", "gout", "gout_pre", "gout_alpha", "gout_part")
+
+
 class UNetEngine:
     """Buffers and prebuilt launch descriptors of one Program (the network, or
     one block) for one input shape (B, H, W of level 0)."""
@@ -649,6 +664,7 @@ class UNetEngine:
         part_need = 0
         for b, L in enumerate(reversed(self.layers)):   # backward order -> ring slot
             L.extra["slot"] = b % self.slots
+            L.extra["bidx"] = b
             L.extra["dyp"] = self.dyp[L.extra["slot"]].data_ptr()
         for L in self.layers:
             olvl = self._out_level(L)
@@ -749,6 +765,7 @@ class UNetEngine:
             L.extra["pidx"] = pidx
             L.extra["goff"] = [4 * self.fp.offsets[i] for i in pidx]   # byte offsets in a flat gradient buffer
             L.extra["olvl"] = olvl
+        part_need = max(part_need, self._plan_gate_out())
         self.ws = torch.zeros(max(ws_need // 4, 4), dtype=torch.float32, device=self.device)
         # fused layers write their slabs from the compute stream while the side stream
         # may still reduce an earlier layer's: one workspace per ring slot, released by
@@ -762,12 +779,64 @@ class UNetEngine:
             L.wgrad_desc.ws = self.ws_dw[L.extra["slot"]].data_ptr() if L.extra["dw"] else self.ws.data_ptr()
             if L.extra["fused"]:
                 L.wgrad_desc.part = L.extra["pws"]
+        for L in self.layers:   # the finisher's epilogue writes the gated layer's partials
+            K = L.extra.get("gates")
+            if K is not None:
+                L.dgrad_desc.gout_part = K.extra["pws"]
         if self.side is not None:   # per layer: dYpre ready (compute stream) / slot free (side stream)
             for L in self.layers:
                 L.extra["ev_ready"] = torch.cuda.Event()
                 L.extra["ev_done"] = torch.cuda.Event()
             self.ev_begin = torch.cuda.Event()
             self.ev_end = torch.cuda.Event()
+
+    def _plan_gate_out(self) -> int:
+        """Pair every layer that still needs a separate PReLU-backward pass with the
+        last consumer of its output in backward order when that consumer's input
+        gradient has the layer's output as the tail of its columns (dense conv_k+1
+        for slice out_k, Unet_model.py:81-87; up_l.conv for up_l.conv_t's output,
+        :43), and let that epilogue write the layer's dYpre and dalpha/dbias
+        partials (rdn_conv_desc.gout).  Returns the partial-workspace bytes needed."""
+        if not GATE_OUT:
+            return 0
+        lib = H.lib()
+        need = 0
+        index = {id(L): i for i, L in enumerate(self.layers)}
+        for K in self.layers:
+            # (level 0: the finisher's 8-byte-per-lane epilogue streams the extra PReLU
+            # input slower than the separate pass does -- up_0: +13 us per step)
+            if (K.extra["fused"] or K.dst is None or K.kind == "down" or K.cout != K.cout_pad
+                    or self._out_level(K) == 0):
+                continue
+            lo, hi = K.dst.c0, K.dst.c0 + K.cout
+            cons = [L for L in self.layers if index[id(L)] > index[id(K)] and L.src.buf == K.dst.buf
+                    and L.src.c0 < hi and L.src.c0 + L.cin > lo]
+            # a residual reader of the slice adds its gradient in another epilogue: not here
+            resid = any(L.resid is not None and L.resid.buf == K.dst.buf and L.resid.c0 < hi
+                        and L.resid.c0 + L.resid_c > lo for L in self.layers)
+            if not cons or resid:
+                continue
+            J = min(cons, key=lambda L: index[id(L)])   # last in backward order
+            if (J.kind != "c3" or J.extra["dw"] or J.extra.get("gates") is not None or J.src.buf in self.pure_inputs
+                    or J.cin != J.cin_pad or J.src.c0 + J.cin != hi or J.src.c0 > lo):
+                continue
+            pre = self.bufs[K.pre]
+            d = J.dgrad_desc
+            d.gout, d.gout_ps = K.extra["dyp"], K.cout_pad
+            d.gout_pre, d.gout_pre_ps = pre.data_ptr(), pre.shape[1]
+            d.gout_alpha = self.named[K.act + ".weight"].data_ptr()
+            d.gout_part = 4096   # stand-in until the workspace exists (rows probe)
+            d.gout_c0 = lo - J.src.c0
+            rows = lib.rdn_conv_gate_rows(C.byref(d))
+            if rows <= 0:
+                d.gout = d.gout_pre = d.gout_alpha = d.gout_part = None
+                d.gout_ps = d.gout_pre_ps = d.gout_c0 = 0
+                continue
+            J.extra["gates"] = K
+            K.extra["gated_by"] = J
+            K.extra["part_rows"] = rows
+            need = max(need, rows * 2 * K.cout * 4)
+        return need
 
     @staticmethod
     def _probe_copy(desc, cls, keep):
@@ -783,7 +852,7 @@ class UNetEngine:
     def _kernel_key(self, desc):
         """Name of the kernel instantiation a conv descriptor launches, as the
         library's own dispatch decides it (rdn_conv_kernel_name)."""
-        d = self._probe_copy(desc, H.ConvDesc, ("gate", "gate_alpha"))
+        d = self._probe_copy(desc, H.ConvDesc, _CONV_SELECT)
         buf = C.create_string_buffer(128)
         H.check(H.lib().rdn_conv_kernel_name(C.byref(d), buf, 128), "rdn_conv_kernel_name")
         return buf.value.decode()
@@ -795,7 +864,7 @@ class UNetEngine:
         return buf.value.decode()
 
     def _dw_key(self, d, wg):
-        dc = self._probe_copy(d, H.ConvDesc, ("gate", "gate_alpha"))
+        dc = self._probe_copy(d, H.ConvDesc, _CONV_SELECT)
         wc = self._probe_copy(wg, H.WgradDesc, ("a_gate", "a_gate_alpha", "part"))
         buf = C.create_string_buffer(128)
         H.check(H.lib().rdn_conv_dgrad_wgrad_kernel_name(C.byref(dc), C.byref(wc), buf, 128),
@@ -821,7 +890,8 @@ class UNetEngine:
                 # a fused PReLU backward (gate in the loader) also reads the saved
                 # PReLU input of the output slice
                 gate = Pout * L.cout if L.extra.get("fused") else 0
-                dg_bytes = es * (Pout * L.cout + gate + Pin * L.cin * (2 if L.accum else 1) +
+                gout = Pin * L.extra["gates"].cout if L.extra.get("gates") is not None else 0
+                dg_bytes = es * (Pout * L.cout + gate + Pin * L.cin * (2 if L.accum else 1) + gout +
                                  (Pin * L.resid_c if L.resid is not None else 0))
                 info["dgrad"] = ("dgrad", L.name, self._kernel_key(L.dgrad_desc), 2 * macs, dg_bytes)
                 info["wgrad"] = ("wgrad", L.name, self._wgrad_key(L.wgrad_desc), 2 * macs,
@@ -921,8 +991,9 @@ class UNetEngine:
             fused = L.extra["fused"]
             dyp, pws = L.extra["dyp"], L.extra["pws"]
             # unfused: the PReLU-backward pass leaves its dalpha/dbias partials in
-            # pws for this layer's rdn_wgrad_reduce to sum (no finalize launch)
-            if fused:
+            # pws for this layer's rdn_wgrad_reduce to sum (no finalize launch);
+            # gated-out: the previous layer's dgrad epilogue already did (below)
+            if fused or "gated_by" in L.extra:
                 rc = 0
             else:
                 if side is not None and b >= self.slots:
@@ -956,6 +1027,10 @@ class UNetEngine:
             else:
                 if side is not None:
                     L.extra["ev_ready"].record(main)
+                K = L.extra.get("gates")
+                if K is not None and side is not None and K.extra["bidx"] >= self.slots:
+                    # this epilogue writes K's dYpre / partials into K's ring slot
+                    main.wait_event(rev[K.extra["bidx"] - self.slots].extra["ev_done"])
                 if L.src.buf not in self.pure_inputs or need_buf[L.src.buf]:
                     tok = tr.start(info["dgrad"]) if tr is not None else None
                     rc = lib.rdn_conv_fwd(C.byref(L.dgrad_desc), st)
@@ -979,7 +1054,8 @@ class UNetEngine:
                 if rc:
                     H.check(rc, f"wgrad[{L.name}]")
             splits, mdim, ndim, ndim_real, taps = L.extra["wgrad"]
-            part_splits = 0 if fused else lib.rdn_prelu_bwd_blocks(self.code, P, L.cout_pad)
+            part_splits = (0 if fused else L.extra["part_rows"] if "gated_by" in L.extra
+                           else lib.rdn_prelu_bwd_blocks(self.code, P, L.cout_pad))
             ow, ob, oa = L.extra["goff"]
             rc = lib.rdn_wgrad_reduce(L.wgrad_desc.ws, splits, mdim, ndim, ndim_real, taps, gbase + ow, 1, pws,
                                       part_splits, gbase + oa, gbase + ob, rst)
