@@ -51,7 +51,12 @@ constexpr int LDS_MAX = 160 * 1024;
 
 template <int BM, int CK>
 struct Geo {
-  static constexpr int NW = 4, NTH = 256;                // waves per block (one per SIMD)
+  // waves per block: 8 (two per SIMD, 64 x 72 wave tiles, 218 VGPRs) for the 64 x 64
+  // level-2/3 shapes -- while one wave issues its LDS-DMA pieces or waits on LDS the
+  // other multiplies: 6-8 % faster per launch (scripts/wg_kbench.py,
+  // profiles/r03_v10_wgrad_glds_diag.txt); 4 (one per SIMD) elsewhere (the 80- and
+  // 96-column groups spill at two waves per SIMD)
+  static constexpr int NW = (BM == 64 && CK == 64) ? 8 : 4, NTH = 64 * NW;
   static constexpr int NCOL = 9 * CK, NT_ALL = (NCOL + 15) / 16;
   // waves as WMv (along M) x WNv (along the 9*CK columns), the same number of
   // n-tiles for every wave (a wave-dependent trip count costs accumulator copies);
@@ -67,7 +72,7 @@ struct Geo {
   static constexpr int HPW = (HPC + NW - 1) / NW;
   static constexpr int B_OFF = A_PIECES * 1024;
   static constexpr int STAGE = B_OFF + HPC * 1024;
-  static constexpr int NS = 3 * STAGE <= LDS_MAX ? 3 : 2;
+  static constexpr int NS = 3 * STAGE <= LDS_MAX ? 3 : 2;   // (4 stages where they fit: no change, r03)
   static constexpr bool OK = NS * STAGE <= LDS_MAX && MTW >= 1;
   static_assert(A_PIECES % NW == 0 && CK % 8 == 0, "image geometry");
 };
@@ -87,16 +92,22 @@ __device__ __forceinline__ int rot(int x) {
 template <int N>
 __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
-// DMAs wave w issues per tile: PA_ dY pieces + halo pieces w, w+4, ... < HPC
-template <int PA_, int HPC>
-__device__ __forceinline__ void wait_own(int wave, bool one_ahead) {
-  if (!one_ahead) { wait_vm<0>(); return; }
-  switch (wave) {
-    case 0: wait_vm<PA_ + (HPC + 3) / 4>(); break;
-    case 1: wait_vm<PA_ + (HPC + 2) / 4>(); break;
-    case 2: wait_vm<PA_ + (HPC + 1) / 4>(); break;
-    default: wait_vm<PA_ + HPC / 4>(); break;
+// DMAs wave w issues per tile: PA_ dY pieces + halo pieces w, w+4, ... < HPC;
+// wait until at most `ahead` later tiles of this wave's DMAs are in flight
+template <int PA_, int HPC, int NW, int K, int W = 0>
+__device__ __forceinline__ void wait_own_k(int wave) {   // wave w issues PA_ + (HPC - w + NW - 1) / NW per tile
+  if constexpr (W < NW - 1) {
+    if (wave == W) { wait_vm<K * (PA_ + (HPC + NW - 1 - W) / NW)>(); return; }
+    wait_own_k<PA_, HPC, NW, K, W + 1>(wave);
+  } else {
+    wait_vm<K * (PA_ + (HPC + NW - 1 - W) / NW)>();
   }
+}
+template <int PA_, int HPC, int NW>
+__device__ __forceinline__ void wait_own(int wave, int ahead) {
+  if (ahead <= 0) wait_vm<0>();
+  else if (ahead == 1) wait_own_k<PA_, HPC, NW, 1>(wave);
+  else wait_own_k<PA_, HPC, NW, 2>(wave);
 }
 
 // One LDS-DMA wave-instruction: 16 B per lane from `src` to LDS byte dst + lane*16
@@ -117,7 +128,7 @@ __device__ __forceinline__ unsigned lds_addr(const unsigned char* p) {
 }
 
 template <int BM, int CK>
-__global__ __launch_bounds__(256, 1) void wgrad3_glds_kernel(rdn_wgrad_desc d, int tiles_x, int tiles_y, int ntiles,
+__global__ __launch_bounds__((Geo<BM, CK>::NTH), 1) void wgrad3_glds_kernel(rdn_wgrad_desc d, int tiles_x, int tiles_y, int ntiles,
                                                              int tiles_per_block) {
   using G_ = Geo<BM, CK>;
   constexpr int RA = G_::RA, RB = G_::RB, UA = G_::UA, UB = G_::UB, NW = G_::NW, MTW = G_::MTW, NTW = G_::NTW;
@@ -220,6 +231,13 @@ __global__ __launch_bounds__(256, 1) void wgrad3_glds_kernel(rdn_wgrad_desc d, i
     // SIMD, so nothing else hides the LDS latency
     bf16x8 af[2][MTW], bfr[2][NTW];
     auto ld = [&](int ks, int buf) {
+#ifdef WG_DIAG_NO_LDS   // diagnostic build (scripts/wg_kbench.py): opaque operands, no LDS reads
+#pragma unroll
+      for (int i = 0; i < MTW; ++i) asm volatile("" : "=v"(af[buf][i]));
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) asm volatile("" : "=v"(bfr[buf][j]));
+      return;
+#endif
 #pragma unroll
       for (int i = 0; i < MTW; ++i) {
         const unsigned char* a = st + aoff[i] + ks * 32 * RA;
@@ -240,11 +258,18 @@ __global__ __launch_bounds__(256, 1) void wgrad3_glds_kernel(rdn_wgrad_desc d, i
     for (int ks = 0; ks < TP / 32; ++ks) {
       if (ks + 1 < TP / 32) ld(ks + 1, (ks + 1) & 1);
       __builtin_amdgcn_sched_barrier(0);
+#ifdef WG_DIAG_NO_MFMA   // diagnostic build: fragments consumed without MFMAs
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) asm volatile("" ::"v"(bfr[ks & 1][j]));
+#pragma unroll
+      for (int i = 0; i < MTW; ++i) asm volatile("" ::"v"(af[ks & 1][i]));
+#else
 #pragma unroll
       for (int j = 0; j < NTW; ++j)
 #pragma unroll
         for (int i = 0; i < MTW; ++i)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks & 1][i], bfr[ks & 1][j], acc[i][j], 0, 0, 0);
+#endif
     }
   };
 
@@ -254,22 +279,37 @@ __global__ __launch_bounds__(256, 1) void wgrad3_glds_kernel(rdn_wgrad_desc d, i
     if (k < t_cnt) issue(t_beg + k, k);
   auto step = [&](int it, auto S) {
     constexpr int s = decltype(S)::value;
-    // own DMAs of tile it landed (with NS = 3 tile it+1 may still fly)
-    wait_own<PA, HPC>(wave, NS == 3 && it + 1 < t_cnt);
+    // own DMAs of tile it landed (tiles it+1 .. it+NS-2 may still fly)
+    wait_own<PA, HPC, NW>(wave, min(NS - 2, t_cnt - 1 - it));
     __builtin_amdgcn_s_barrier();           // everyone's landed; everyone done reading tile it-1's stage
     asm volatile("" ::: "memory");
+#ifndef WG_DIAG_NO_DMA   // diagnostic build: only the prologue's tiles are loaded
     if (it + NS - 1 < t_cnt) issue(t_beg + it + NS - 1, (s + NS - 1) % NS);
+#endif
     compute(s);
   };
   for (int it = 0; it < t_cnt; it += NS) {
     step(it, std::integral_constant<int, 0>{});
     if (it + 1 < t_cnt) step(it + 1, std::integral_constant<int, 1 % NS>{});
-    if constexpr (NS == 3)
+    if constexpr (NS >= 3)
       if (it + 2 < t_cnt) step(it + 2, std::integral_constant<int, 2 % NS>{});
+    if constexpr (NS >= 4)
+      if (it + 3 < t_cnt) step(it + 3, std::integral_constant<int, 3 % NS>{});
   }
 
   // D[m][n]: row = g*4 + e (output channel), col = li (tile column)
   const int ncol_all = 9 * d.ndim;
+#ifdef WG_DIAG_NO_EPI   // diagnostic build: one store per lane keeps the accumulators live
+  {
+    float t = 0.f;
+#pragma unroll
+    for (int j = 0; j < NTW; ++j)
+#pragma unroll
+      for (int i = 0; i < MTW; ++i) t += acc[i][j][0] + acc[i][j][3];
+    if (t == 1.2345f) d.ws[threadIdx.x] = t;
+    return;
+  }
+#endif
   float* __restrict__ ws = d.ws + (int64_t)bz * d.mdim * ncol_all;
 #pragma unroll
   for (int j = 0; j < NTW; ++j) {
@@ -293,7 +333,7 @@ int launch(const rdn_wgrad_desc* d, int blocks, int tiles_x, int tiles_y, int nt
   if constexpr (Geo<BM, CK>::OK) {
     if (!d->a_gate) {
       RDN_PROBE("wgrad3_glds_kernel<bf16,%d,%d>", BM, CK);
-      wgrad3_glds_kernel<BM, CK><<<blocks, 256, 0, st>>>(*d, tiles_x, tiles_y, ntiles, tpb);
+      wgrad3_glds_kernel<BM, CK><<<blocks, Geo<BM, CK>::NTH, 0, st>>>(*d, tiles_x, tiles_y, ntiles, tpb);
       return rdn_check_launch("rdn_conv_wgrad(conv3 glds)");
     }
   }

@@ -579,7 +579,9 @@ Plan plan(const rdn_wgrad_desc* d) {
     const int base = p.mtiles * p.chunks;
     // blocks per launch: 192 of the 256 CUs, leaving room beside the dgrad chain;
     // step A/B (3 interleaved rounds, same box): 128: 1483, 192: 1506, 256: 1499,
-    // 512: 1416 img/s (past 256 the 1-per-CU blocks run in two waves)
+    // 512: 1416 img/s (past 256 the 1-per-CU blocks run in two waves); re-measured in
+    // r03 (profiles/r03_v10_wglds_blocks_ab.txt): 96: 1633, 128: 1698, 160: 1714,
+    // 192: 1714, 256: 1687
     constexpr int gtarget = 192;
     int s = d->splits > 0 ? d->splits : gtarget / base;
     const int maxs = (p.ntiles + 1) / 2;                             // >= 2 tiles per block
