@@ -227,8 +227,12 @@ __global__ __launch_bounds__((Geo<BM, CK>::NTH), 1) void wgrad3_glds_kernel(rdn_
 
   auto compute = [&](int stage) {
     const unsigned char* const st = lds + stage * G_::STAGE;
-    // all fragments of k-step ks+1 are read before the MFMAs of ks: one wave per
-    // SIMD, so nothing else hides the LDS latency
+    // all fragments of k-step ks+1 are read before the MFMAs of ks (at one wave per
+    // SIMD nothing else hides the LDS latency; spreading the reads between the MFMAs
+    // with sched_group_barrier gained 2-3 %, r03).  Where this wave's time goes (the
+    // -DWG_DIAG_* builds, L2 conv_3 at B16): MFMAs alone 38.6 us, + LDS reads 51.2,
+    // + LDS-DMA 56.7, everything 66.9 -- the DMA issue and the fragment reads, not the
+    // MFMAs, are what the second wave per SIMD (NW = 8) partly hides
     bf16x8 af[2][MTW], bfr[2][NTW];
     auto ld = [&](int ks, int buf) {
 #ifdef WG_DIAG_NO_LDS   // diagnostic build (scripts/wg_kbench.py): opaque operands, no LDS reads

@@ -187,9 +187,13 @@ FUSE_PRELU = os.environ.get("RDN_FUSE_PRELU", "1") != "0"
 # weight gradients on a side stream (overlapped with the dgrad chain) and the depth
 # of the dYpre ring that decouples the two chains
 WGRAD_STREAM = os.environ.get("RDN_WGRAD_STREAM", "1") != "0"
-# (6 slots: 1690 / 1691 img/s against 1672 / 1673 with 4, 1681-1684 with 8, 1678-1682
-# with 12; interleaved on one box, profiles/r03_v9_slots_ab.txt)
-WGRAD_SLOTS = int(os.environ.get("RDN_WGRAD_SLOTS", "6"))
+# (a ring of 6 slots: 1690 / 1691 img/s against 1672 / 1673 with 4, 1681-1684 with 8,
+# 1678-1682 with 12, profiles/r03_v9_slots_ab.txt; one slot per layer -- no dgrad-chain
+# waits on the weight-gradient stream at all, each a ~6 us cross-queue gap in the
+# replayed graph -- 1739 / 1742 against 1723 / 1724 with 6, profiles/r03_v11_slots_ab.txt;
+# all interleaved on one box.  Memory: the dYpre / partial / slab buffers of every layer,
+# ~1.5 GB at B16)
+WGRAD_SLOTS = int(os.environ.get("RDN_WGRAD_SLOTS", "0"))   # 0: one slot per layer
 # bench.py's per-kernel profiling pass serialises the backward (isolated kernel times)
 SERIAL_BWD = False
 # channel-blocked ("planar") activation buffers: a level-l buffer is [C/cb, P, cb] with
@@ -585,15 +589,19 @@ class UNetEngine:
                     continue
                 alloc("d" + name, lvl, ch)
             # weight gradients (wgrad + reduce) run on a side stream, overlapped with
-            # the dgrad chain; the per-layer dYpre / PReLU-partial buffers they read
-            # form a ring of SLOTS so the dgrad chain can run SLOTS layers ahead
+            # the dgrad chain; the dYpre / PReLU-partial / slab buffers they read live in
+            # SLOTS slots (layer b of the backward order uses slot b % SLOTS), each sized
+            # for the largest layer that uses it; the dgrad chain waits for the side
+            # stream only where it reuses a slot (default: one slot per layer, no waits)
             self.side = torch.cuda.Stream(device=dev) if (dev.type == "cuda" and WGRAD_STREAM) else None
-            self.slots = WGRAD_SLOTS if self.side is not None else 1
-            self.dyp_elems = max(self.P[self._out_level(L)] * L.cout_pad for L in layers)
-            self.dyp = torch.zeros(self.slots, self.dyp_elems, dtype=dtype, device=dev)
-            lib = H.lib()
-            self.pws_bytes = max(lib.rdn_prelu_bwd_workspace_size(self.code, self.P[self._out_level(L)], L.cout,
-                                                                  L.cout_pad) for L in layers)
+            if self.side is None:
+                self.slots = 1
+            else:
+                self.slots = len(layers) if WGRAD_SLOTS <= 0 else min(WGRAD_SLOTS, len(layers))
+            sizes = [0] * self.slots
+            for b, L in enumerate(reversed(layers)):
+                sizes[b % self.slots] = max(sizes[b % self.slots], self.P[self._out_level(L)] * L.cout_pad)
+            self.dyp = [torch.zeros(n, dtype=dtype, device=dev) for n in sizes]
             self._build_bwd()
         self._build_info()
         self.lease = None   # weakref to the autograd graph's lease while it owns the activations
@@ -660,8 +668,6 @@ class UNetEngine:
     def _build_bwd(self):
         lib = H.lib()
         ws_need = 0
-        dw_need = 0
-        part_need = 0
         for b, L in enumerate(reversed(self.layers)):   # backward order -> ring slot
             L.extra["slot"] = b % self.slots
             L.extra["bidx"] = b
@@ -752,28 +758,34 @@ class UNetEngine:
             if fused and FUSE_DW and L.src.buf not in self.pure_inputs:
                 dw = lib.rdn_conv_dgrad_wgrad_splits(C.byref(d), C.byref(wg))
             L.extra["dw"] = dw > 0
+            L.extra["dw_bytes"] = 0
             if dw > 0:   # the fused kernel's slabs: one per block of its persistent grid
                 splits = wg.splits = dw
-                dw_need = max(dw_need, dw * wg.mdim * 9 * wg.ndim * 4)
+                L.extra["dw_bytes"] = dw * wg.mdim * 9 * wg.ndim * 4
             else:
                 ws_need = max(ws_need, lib.rdn_wgrad_workspace_size(C.byref(wg)))
-            if fused:
-                part_need = max(part_need, splits * 2 * wg.mdim * 4)
+            # dalpha / dbias partials: the fused loaders' per-split rows, else the
+            # separate PReLU-backward pass's per-block rows
+            L.extra["part_bytes"] = (splits * 2 * wg.mdim * 4 if fused else
+                                     lib.rdn_prelu_bwd_workspace_size(self.code, self.P[olvl], L.cout, L.cout_pad))
             L.wgrad_desc = wg
             L.extra["wgrad"] = (splits, wg.mdim, wg.ndim, ndim_real, taps)
             pidx = [self.fp.index[n] for n in (L.name + ".weight", L.name + ".bias", L.act + ".weight")]
             L.extra["pidx"] = pidx
             L.extra["goff"] = [4 * self.fp.offsets[i] for i in pidx]   # byte offsets in a flat gradient buffer
             L.extra["olvl"] = olvl
-        part_need = max(part_need, self._plan_gate_out())
+        self._plan_gate_out()
         self.ws = torch.zeros(max(ws_need // 4, 4), dtype=torch.float32, device=self.device)
-        # fused layers write their slabs from the compute stream while the side stream
-        # may still reduce an earlier layer's: one workspace per ring slot, released by
-        # the same ev_done wait that releases the slot's partials
-        self.ws_dw = (torch.zeros(self.slots, (dw_need // 4 + 3) // 4 * 4, dtype=torch.float32, device=self.device)
-                      if dw_need else None)
-        pws = max(part_need, self.pws_bytes, 16) // 4
-        self.pws = torch.zeros(self.slots, (pws + 3) // 4 * 4, dtype=torch.float32, device=self.device)
+        # per slot: fused layers' slabs (written from the compute stream while the side
+        # stream may still reduce an earlier layer's) and the dalpha/dbias partials
+        dwb, pwb = [0] * self.slots, [16] * self.slots
+        for L in self.layers:
+            sl = L.extra["slot"]
+            dwb[sl] = max(dwb[sl], L.extra["dw_bytes"])
+            pwb[sl] = max(pwb[sl], L.extra["part_bytes"])
+        f32 = dict(dtype=torch.float32, device=self.device)
+        self.ws_dw = [torch.zeros((n // 4 + 3) // 4 * 4, **f32) if n else None for n in dwb]
+        self.pws = [torch.zeros((n // 4 + 3) // 4 * 4, **f32) for n in pwb]
         for L in self.layers:
             L.extra["pws"] = self.pws[L.extra["slot"]].data_ptr()
             L.wgrad_desc.ws = self.ws_dw[L.extra["slot"]].data_ptr() if L.extra["dw"] else self.ws.data_ptr()
@@ -835,6 +847,7 @@ class UNetEngine:
             J.extra["gates"] = K
             K.extra["gated_by"] = J
             K.extra["part_rows"] = rows
+            K.extra["part_bytes"] = max(K.extra["part_bytes"], rows * 2 * K.cout * 4)
             need = max(need, rows * 2 * K.cout * 4)
         return need
 
