@@ -444,7 +444,7 @@ def dense_conv_path(prof, batch):
     import re
     byts, ms, n = 0.0, 0.0, 0
     for info, s, e in prof.records:
-        m = re.match(r"block_(\d)_\d\.conv_\d$", info[1])
+        m = re.match(r"block_(\d)_\d\.conv_[\d-]+$", info[1])   # (conv_0-2: the fused level-0 launch)
         if m and int(m.group(1)) in DENSE_LEVELS:
             byts += info[4]
             ms += s.elapsed_time(e)

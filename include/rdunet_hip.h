@@ -25,6 +25,8 @@
  *   rdn_conv_wgrad /  aten convolution_backward grad_weight for the same convs.
  *   rdn_wgrad_reduce
  *   rdn_conv_dgrad_wgrad  both of the above for one gated level-0 conv in one pass.
+ *   rdn_dense3_fwd    conv_0..conv_2 (+ PReLU, + torch.cat) of a level-0 DenoisingBlock
+ *                     in one pass, Unet_model.py:81-87.
  *   rdn_prelu_bwd     aten _prelu_kernel_backward (dx, dalpha) + conv grad_bias.
  *   rdn_interp        x = a*noisy + (1-a)*clean, diffusion_RDUnet.py:90-100, :33-36.
  *   rdn_pack_input    torch.cat((inputs, t.expand(...)), 1), Unet_model.py:135-136.
@@ -174,6 +176,23 @@ int rdn_conv_dgrad_wgrad(const rdn_conv_desc* dgrad, const rdn_wgrad_desc* wgrad
 int rdn_conv_dgrad_wgrad_splits(const rdn_conv_desc* dgrad, const rdn_wgrad_desc* wgrad);
 /* name of the fused kernel instantiation (1 = not served) */
 int rdn_conv_dgrad_wgrad_kernel_name(const rdn_conv_desc* dgrad, const rdn_wgrad_desc* wgrad, char* buf, int32_t len);
+
+/* Fused forward of conv_0..conv_2 of a level-0 DenoisingBlock with base_filters 32
+   (Unet_model.py:81-87: x 32 channels, growth 16, bf16): the same results as the three
+   rdn_conv_fwd launches (bias, PReLU-input store, PReLU), in one pass that reads x once
+   and keeps out_0 / out_1 on chip.  x: the block buffer's first plane (channels 0-15;
+   channels 16-31 x_pl elements further; channel-blocked, 16-channel planes);
+   out[k]: the plane receiving conv_k's output (pixel stride 16); pre[k]: its PReLU
+   input, plain [pixels][16]; wp[k]: packed forward weights (rdn_pack_weights with
+   ck = cin, kp[k] columns).  H % 8 == 0, W % 16 == 0. */
+typedef struct rdn_dense3_desc {
+  int32_t n, h, w;
+  const void* x; int64_t x_pl;
+  void* out[3]; void* pre[3];
+  const void* wp[3]; int32_t kp[3];
+  const float* bias[3]; const float* alpha[3];
+} rdn_dense3_desc;
+int rdn_dense3_fwd(const rdn_dense3_desc* d, void* stream);
 
 /* PReLU backward (+ conv bias gradient) over a pixel grid of `pixels` pixels:
    dyp[p, c] = dy[p, c] * (pre[p, c] > 0 ? 1 : alpha[c])   (c < C; 0 for C <= c < cpad)

@@ -1,0 +1,47 @@
+"""Fused forward of conv_0..conv_2 of the level-0 DenoisingBlocks (rdn_dense3_fwd,
+csrc/conv3_dense.hip; Unet_model.py:81-87) against the three rdn_conv_fwd launches it
+replaces.  The fused kernel multiplies the same bf16 operands in the same k order
+(tap-major, channel-minor, 32-deep MFMA steps) and rounds out_0 / out_1 to bf16
+before conv_1 / conv_2 read them, exactly as the HBM round trip does, so the network
+output, every saved PReLU input and therefore every gradient are bit-identical.
+Shapes: the train step's 256^2, a small image whose tiles all touch the border, and a
+non-square one."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(fuse, B, Hh, Ww, seed=0):
+    import vub_image_denoising_amd as vm
+    from vub_image_denoising_amd import engine as E
+    old = E.FUSE_DENSE
+    E.FUSE_DENSE = fuse
+    try:
+        torch.manual_seed(seed)
+        m = vm.RDUNet_T(base_filters=32).cuda()
+        m.set_compute_dtype("bf16")
+        g = torch.Generator().manual_seed(seed + 1)
+        x = (torch.rand(B, 3, Hh, Ww, generator=g) * 2 - 1).cuda()
+        t = torch.rand(B, 1, 1, 1, generator=g).cuda()
+        w = torch.randn(B, 3, Hh, Ww, generator=g).cuda()
+        y = m(x, t)
+        (y * w).mean().backward()
+        grads = {n: p.grad.detach().clone() for n, p in m.named_parameters()}
+        fused = sum("dense3" in L.extra for pool in m._rdn_engines.values() for eng in pool for L in eng.layers)
+        with torch.no_grad():   # inference engine (no PReLU inputs kept)
+            y_inf = m(x, t)
+        return y.detach().clone(), y_inf, grads, fused
+    finally:
+        E.FUSE_DENSE = old
+
+
+@pytest.mark.parametrize("B,Hh,Ww", [(2, 256, 256), (1, 64, 64), (2, 40, 48)])
+def test_dense3_bit_identical(B, Hh, Ww):
+    y0, yi0, g0, n0 = _run(False, B, Hh, Ww)
+    y1, yi1, g1, n1 = _run(True, B, Hh, Ww)
+    assert n0 == 0 and n1 == 4, (n0, n1)
+    assert torch.equal(y0, y1)
+    assert torch.equal(yi0, yi1)
+    for n in g0:
+        assert torch.equal(g0[n], g1[n]), n

@@ -54,6 +54,16 @@ class WgradDesc(C.Structure):
     ]
 
 
+class Dense3Desc(C.Structure):
+    _fields_ = [
+        ("n", _i32), ("h", _i32), ("w", _i32),
+        ("x", _vp), ("x_pl", _i64),
+        ("out", _vp * 3), ("pre", _vp * 3),
+        ("wp", _vp * 3), ("kp", _i32 * 3),
+        ("bias", _vp * 3), ("alpha", _vp * 3),
+    ]
+
+
 class PackItem(C.Structure):
     _fields_ = [("w", _vp), ("out", _vp), ("mode", _i32), ("d0", _i32), ("d1", _i32), ("kh", _i32), ("kw", _i32),
                 ("pad0", _i32), ("pad1", _i32), ("rows_pad", _i32), ("kp", _i32), ("ck", _i32)]
@@ -76,6 +86,7 @@ SIGNATURES = {
     "rdn_conv_dgrad_wgrad_splits": (_i32, [C.POINTER(ConvDesc), C.POINTER(WgradDesc)]),
     "rdn_conv_dgrad_wgrad_kernel_name": (_i32, [C.POINTER(ConvDesc), C.POINTER(WgradDesc), C.c_char_p, _i32]),
     "rdn_wgrad_chunks": (_i32, [C.POINTER(WgradDesc)]),
+    "rdn_dense3_fwd": (_i32, [C.POINTER(Dense3Desc), _vp]),
     "rdn_wgrad_workspace_size": (_i64, [C.POINTER(WgradDesc)]),
     "rdn_wgrad_reduce": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _vp, _i32, _vp, _i32, _vp, _vp, _vp]),
     "rdn_prelu_bwd_blocks": (_i32, [_i32, _i64, _i32]),

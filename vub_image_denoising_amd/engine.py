@@ -212,6 +212,9 @@ FUSE_DW = os.environ.get("RDN_DW", "1") != "0"
 # profiles/r03_v9_slots_ab.txt): the longer finisher launches sit on the critical path
 # beside the weight-gradient stream.  Tested both ways (tests/test_gpu_gateout.py).
 GATE_OUT = os.environ.get("RDN_GATE_OUT", "0") == "1"
+# conv_0..conv_2 of every level-0 DenoisingBlock (base_filters 32, bf16) as ONE
+# launch that reads x once and keeps out_0 / out_1 on chip (rdn_dense3_fwd)
+FUSE_DENSE = os.environ.get("RDN_DENSE", "1") != "0"
 
 
 def find_flat(params):
@@ -583,6 +586,7 @@ class UNetEngine:
             alloc(name, lvl, ch)
         self.named = dict(module.named_parameters())
         self._build_fwd()
+        self._plan_dense3()
         if train:
             for name, (lvl, ch) in bufspec.items():
                 if name.startswith("PRE_"):
@@ -664,6 +668,52 @@ class UNetEngine:
                     d.res_climit = L.resid_c
             d.flags = flags
             L.fwd_desc = d
+
+    def _plan_dense3(self):
+        """Level-0 dense blocks whose conv_0..conv_2 forward runs as one
+        rdn_dense3_fwd launch (Unet_model.py:81-87 with x = 32 channels, growth 16):
+        the three layers read the block buffer's channel prefix (channel-blocked,
+        16-channel planes) and write its next planes; the launch goes at conv_0, the
+        other two are skipped."""
+        if not FUSE_DENSE or self.code != H.RDN_BF16 or self.H % 8 or self.W % 16:
+            return
+        by_name = {L.name: L for L in self.layers}
+        for L0 in self.layers:
+            if not L0.name.endswith(".conv_0") or L0.kind != "c3" or L0.level != 0:
+                continue
+            blk = L0.name[:-len(".conv_0")]
+            Ls = [by_name.get(f"{blk}.conv_{k}") for k in range(3)]
+            if any(L is None or L.kind != "c3" or L.level != 0 for L in Ls):
+                continue
+            buf = L0.src.buf
+            ps, pl = self.geo[buf]
+            if (ps != 16 or not pl or any(L.src.buf != buf or L.src.c0 != 0 or L.dst is None or L.dst.buf != buf
+                                            or L.cout != 16 or L.cout_pad != 16 or L.resid is not None for L in Ls)
+                    or [L.cin for L in Ls] != [32, 48, 64] or [L.dst.c0 for L in Ls] != [32, 48, 64]):
+                continue
+            d = H.Dense3Desc()
+            n, h, w = self.grid[0]
+            d.n, d.h, d.w = n, h, w
+            d.x, d.x_pl = self.bufs[buf].data_ptr(), pl
+            for k, L in enumerate(Ls):
+                ptr, _, c0, _ = self._slice(L.dst)
+                d.out[k] = ptr + 2 * (c0 // ps) * pl
+                pre = self.bufs.get(L.pre)
+                d.pre[k] = pre.data_ptr() if pre is not None else self._dense_scratch(L.pre)
+                packed = L.pack_fwd[8]
+                d.wp[k], d.kp[k] = packed.data_ptr(), packed.shape[1]
+                d.bias[k] = self.named[L.name + ".bias"].data_ptr()
+                d.alpha[k] = self.named[L.act + ".weight"].data_ptr()
+            L0.extra["dense3"] = d
+            for L in Ls[1:]:
+                L.extra["dense3_skip"] = True
+
+    def _dense_scratch(self, name):
+        """PReLU-input target of a fused launch in an inference engine (no PRE_
+        buffers kept): one shared scratch plane, written and never read."""
+        if not hasattr(self, "_pre_scratch"):
+            self._pre_scratch = torch.empty(self.P[0] * 16, dtype=self.dtype, device=self.device)
+        return self._pre_scratch.data_ptr()
 
     def _build_bwd(self):
         lib = H.lib()
@@ -899,6 +949,8 @@ class UNetEngine:
             fwd_bytes = es * (Pin * L.cin + Pout * L.cout * (2 if self.train else 1) +
                               (Pout * L.cout if L.resid is not None else 0))
             info = {"fwd": ("fwd", L.name, self._kernel_key(L.fwd_desc), 2 * macs, fwd_bytes)}
+            if "dense3" in L.extra:   # conv_0..2 in one launch: their algorithmic work summed below
+                info["dense3"] = None
             if self.train:
                 # a fused PReLU backward (gate in the loader) also reads the saved
                 # PReLU input of the output slice
@@ -913,6 +965,15 @@ class UNetEngine:
                     info["dw"] = ("dwgrad", L.name, self._dw_key(L.dgrad_desc, L.wgrad_desc), 4 * macs,
                                   dg_bytes + es * Pin * L.cin)
             L.extra["info"] = info
+        # the fused conv_0..2 launch: the three convs' algorithmic FLOPs and bytes (each
+        # conv's input read once, output + PReLU input written once), as unfused
+        by_name = {L.name: L for L in self.layers}
+        for L in self.layers:
+            if "dense3" in L.extra:
+                blk = L.name[:-len(".conv_0")]
+                parts = [by_name[f"{blk}.conv_{k}"].extra["info"]["fwd"] for k in range(3)]
+                L.extra["info"]["dense3"] = ("fwd", f"{blk}.conv_0-2", "conv3_dense_kernel<bf16,32,16>",
+                                             sum(p[3] for p in parts), sum(p[4] for p in parts))
 
     # ------------------------------------------------------------------
     def forward(self, xs, t: torch.Tensor | None = None) -> torch.Tensor:
@@ -953,8 +1014,11 @@ class UNetEngine:
         fwd = lib.rdn_conv_fwd
         tr = TRACER
         for L in self.layers:
-            tok = tr.start(L.extra["info"]["fwd"]) if tr is not None else None
-            rc = fwd(C.byref(L.fwd_desc), st)
+            if "dense3_skip" in L.extra:
+                continue
+            d3 = L.extra.get("dense3")
+            tok = tr.start(L.extra["info"]["dense3" if d3 is not None else "fwd"]) if tr is not None else None
+            rc = lib.rdn_dense3_fwd(C.byref(d3), st) if d3 is not None else fwd(C.byref(L.fwd_desc), st)
             if tok is not None:
                 tr.stop(tok)
             if rc:
