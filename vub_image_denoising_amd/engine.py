@@ -194,6 +194,14 @@ WGRAD_STREAM = os.environ.get("RDN_WGRAD_STREAM", "1") != "0"
 # all interleaved on one box.  Memory: the dYpre / partial / slab buffers of every layer,
 # ~1.5 GB at B16)
 WGRAD_SLOTS = int(os.environ.get("RDN_WGRAD_SLOTS", "0"))   # 0: one slot per layer
+# With one slot per layer the captured graph has no edge from the weight-gradient branch
+# back into the dgrad chain, and the replay enqueues the whole chain before the branch:
+# harmless while the host enqueues a replay in ~1 ms, but under a profiler (slower
+# enqueue) the branch then ran after the chain (10.3 vs 9.4 ms per step traced,
+# profiles/r03_v13_prof_modes.txt).  Every ORDER_EVERY layers the chain therefore waits
+# for the branch ORDER_EVERY layers back (a few cross-queue edges per step) to pin the
+# replay order.
+ORDER_EVERY = int(os.environ.get("RDN_ORDER_EVERY", "12"))
 # bench.py's per-kernel profiling pass serialises the backward (isolated kernel times)
 SERIAL_BWD = False
 # channel-blocked ("planar") activation buffers: a level-l buffer is [C/cb, P, cb] with
@@ -1066,6 +1074,9 @@ class UNetEngine:
             P = self.P[olvl]
             pre = self.bufs[L.pre]
             fused = L.extra["fused"]
+            if side is not None and ORDER_EVERY and b >= ORDER_EVERY and b % ORDER_EVERY == 0 and b < self.slots:
+                # ordering edge only (no buffer is reused): see ORDER_EVERY
+                main.wait_event(rev[b - ORDER_EVERY].extra["ev_done"])
             dyp, pws = L.extra["dyp"], L.extra["pws"]
             # unfused: the PReLU-backward pass leaves its dalpha/dbias partials in
             # pws for this layer's rdn_wgrad_reduce to sum (no finalize launch);
