@@ -73,6 +73,13 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+#ifndef RDN_PRELU_MINB
+#define RDN_PRELU_MINB 1
+#endif
+#ifndef RDN_PRELU_PU
+#define RDN_PRELU_PU 4
+#endif
+
 static int grid_for(int64_t n, int per_block, int cap = 8192) {
   int64_t b = (n + per_block - 1) / per_block;
   if (b < 1) b = 1;
@@ -85,7 +92,10 @@ static int grid_for(int64_t n, int per_block, int cap = 8192) {
 // (aten prelu backward: mask = input > 0, Activation.cpp; conv grad_bias = sum
 // over N,H,W of grad_output).  Thread = 16-byte channel group of one pixel.
 template <typename T>
-__global__ __launch_bounds__(256) void prelu_bwd_kernel(int64_t pixels, int H, int W, int C, int cpad,
+// (<= 64 VGPRs: one wave per SIMD still fits beside a two-wave weight-gradient block of
+// the side stream -- 2 x 218 of 512 -- so the pass is not confined to the CUs the
+// side stream leaves free)
+__global__ __launch_bounds__(256, RDN_PRELU_MINB) void prelu_bwd_kernel(int64_t pixels, int H, int W, int C, int cpad,
                                                         const T* __restrict__ dy, int64_t dy_ps, int dy_c0,
                                                         int64_t dy_pl, const float* __restrict__ dy_nchw, const T* __restrict__ pre,
                                                         int64_t pre_ps, const float* __restrict__ alpha, T* __restrict__ dyp,
@@ -111,17 +121,17 @@ __global__ __launch_bounds__(256) void prelu_bwd_kernel(int64_t pixels, int H, i
   // (unconditional, from a clamped valid pixel) -- the plain loop exposes one
   // HBM round trip per pixel, which is what the small level-2/3 passes pay
   if (active && !dy_nchw && ((dy_ps | dy_c0) % VEC) == 0) {
-    for (; p0 < pixels; p0 += 4 * stride) {
-      u32x4 gv[4], xv[4];
+    for (; p0 < pixels; p0 += RDN_PRELU_PU * stride) {
+      u32x4 gv[RDN_PRELU_PU], xv[RDN_PRELU_PU];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < RDN_PRELU_PU; ++u) {
         const int64_t pu = p0 + u * stride;
         const int64_t pc = pu < pixels ? pu : p0;
         gv[u] = *(const u32x4*)(dy + pc * dy_ps + dy_cf);
         xv[u] = *(const u32x4*)(pre + pc * pre_ps + grp * VEC);
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < RDN_PRELU_PU; ++u) {
         const int64_t pu = p0 + u * stride;
         if (pu >= pixels) break;
         float g[VEC], x[VEC], o[VEC];
