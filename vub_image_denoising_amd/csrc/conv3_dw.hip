@@ -52,6 +52,12 @@ using c3::TH;
 using c3::TW;
 
 constexpr int NT = 512;   // 8 waves
+#ifndef DW_WPIPE
+#define DW_WPIPE 3   // weight-gradient fragment prefetch depth (0: one k-step at a time)
+#endif
+#ifndef DW_SB
+#define DW_SB 1      // one barrier per tile (dY and X halos double-buffered in LDS)
+#endif
 constexpr int LDS_MAX = 160 * 1024;
 
 template <int BN, int CK>
@@ -73,11 +79,17 @@ struct DwCfg {
   static constexpr int X_IT = (HW_ * (BN / 8) + 255) / 256;
   static constexpr int NTW = (9 * BN / 16 + 3) / 4;
   static constexpr bool DW2 = (CK / 16) * NTW * 4 + 2 * X_IT * 4 <= 112;
-  static constexpr int BASE = W_BYTES + D_BYTES + CT_BYTES + AL_BYTES;
+  // single-barrier schedule: both halos double-buffered in LDS, the D waves' gate
+  // pass overlapping the W waves' MFMAs (per launch, profiles/r03_v15_dw_sb_kbench:
+  // 32->16 59 -> 54 us, 80->32 135 -> 133, 64->32 36 -> 34; the 64->16 and 32->32
+  // shapes ran 1-3 us slower and keep two barriers per tile)
+  static constexpr bool SB = DW_SB && !((BN == 64 && CK == 16) || (BN == 32 && CK == 32));
+  static constexpr int DB = SB ? 2 : 1;
+  static constexpr int BASE = W_BYTES + DB * D_BYTES + CT_BYTES + AL_BYTES;
   // X halo buffers in LDS: 2 for the LDS double buffer, 1 where it would not fit
   // (96 columns were tried: <96,32> spills 128 B in the W loop, so they stay on the
   // separate kernels)
-  static constexpr int XB = DW2 ? 1 : (BASE + 2 * X_BYTES <= LDS_MAX ? 2 : 1);
+  static constexpr int XB = SB ? 2 : DW2 ? 1 : (BASE + 2 * X_BYTES <= LDS_MAX ? 2 : 1);
   static constexpr int LDS = BASE + XB * X_BYTES;
   static constexpr bool FITS = LDS <= LDS_MAX && D_BYTES + X_BYTES + CT_BYTES >= RED_BYTES;
 };
@@ -108,7 +120,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
   __shared__ __attribute__((aligned(16))) unsigned char lds[Cfg::LDS];
   unsigned char* const wl = lds;
   unsigned char* const dyh = lds + Cfg::W_BYTES;
-  unsigned char* const xh = dyh + Cfg::D_BYTES;
+  unsigned char* const xh = dyh + Cfg::DB * Cfg::D_BYTES;
   float* const alds = (float*)(xh + Cfg::XB * Cfg::X_BYTES + Cfg::CT_BYTES);
   float* const red = (float*)(lds + Cfg::W_BYTES);   // partial reduction (aliases the halos after the loops)
 
@@ -210,13 +222,19 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
 #pragma unroll
       for (int it = 0; it < D_IT; ++it) {
         const bool ok = in_img(uhp[it], oy, ox);
+#ifdef DW_DIAG_NO_LOAD
+        lr[it] = u32x4{(unsigned)ok, 0u, 0u, 0u};
+        gr[it] = u32x4{0u, 0u, 0u, 0u};
+        (void)rd; (void)rg;
+#else
         lr[it] = rdn_ld16(rd, ok, lrel[it] * 2);
         gr[it] = rdn_ld16(rg, ok, grel[it] * 2);
+#endif
       }
     };
     // registers -> LDS with the PReLU-backward gate and the dalpha/dbias partials of
     // the tile-interior pixels (each image pixel is interior to exactly one tile)
-    auto store = [&](const u32x4 (&lr)[D_IT], const u32x4 (&gr)[D_IT], bool live) {
+    auto store = [&](const u32x4 (&lr)[D_IT], const u32x4 (&gr)[D_IT], bool live, int doff) {
       const f32x4 a0 = *(const f32x4*)(alds + dcu * VEC), a1 = *(const f32x4*)(alds + dcu * VEC + 4);
 #pragma unroll
       for (int it = 0; it < D_IT; ++it) {
@@ -232,7 +250,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
           dy[q] = pos ? dy[q] : (q < 4 ? a0[q] : a1[q - 4]) * dy[q];
           if (in) sb[q] += dy[q];
         }
-        *(u32x4*)(dyh + llds[it]) = Unit16<bf16>::pack(dy);
+        *(u32x4*)(dyh + doff + llds[it]) = Unit16<bf16>::pack(dy);
       }
     };
     auto load_epi = [&](int tt, u32x2 (&eo)[MT][NTL]) {
@@ -243,7 +261,11 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int jn = 0; jn < NTL; ++jn)
+#ifdef DW_DIAG_NO_LOAD
+          eo[i][jn] = u32x2{0u, 0u};
+#else
           eo[i][jn] = rdn_ld8(rb, eok[jn], (((2 * rw + i) * W + r) * eps + coff_e[jn]) * 2);
+#endif
     };
     // fragments: pixel r of tile rows 2 rw (+1); k-step j covers k = 32 j + 8 g
     const int a_lane = (2 * rw * RS + r) * DROW;
@@ -260,7 +282,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     }
     const unsigned char* const pda = dyh + (KALIGN ? a_lane + g * 16 : 0);
     const unsigned char* const pdb = wl + r * WROW + g * 16;
-    auto dgrad_tile = [&](int tt, const u32x2 (&eo)[MT][NTL]) {
+    auto dgrad_tile = [&](int tt, const u32x2 (&eo)[MT][NTL], int doff) {
       f32x4 acc[MT][NTL];
 #pragma unroll
       for (int i = 0; i < MT; ++i)
@@ -280,16 +302,20 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
         }
         u32x4 fa[MT], fb[NTL];
 #pragma unroll
-        for (int i = 0; i < MT; ++i) fa[i] = *(const u32x4*)(pda + ao + i * RS * DROW);
+        for (int i = 0; i < MT; ++i) fa[i] = *(const u32x4*)(pda + doff + ao + i * RS * DROW);
 #pragma unroll
         for (int jn = 0; jn < NTL; ++jn) fb[jn] = *(const u32x4*)(pdb + jn * 16 * WROW + j * 64);
 #pragma unroll
         for (int i = 0; i < MT; ++i)
 #pragma unroll
           for (int jn = 0; jn < NTL; ++jn)   // D^T[m = column][n = pixel]
+#ifdef DW_DIAG_NO_MFMA
+            acc[i][jn][0] += __builtin_bit_cast(float, fb[jn][0] ^ fa[i][0]);
+#else
             acc[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fb[jn]),
                                                                  __builtin_bit_cast(bf16x8, fa[i]), acc[i][jn], 0,
                                                                  0, 0);
+#endif
       }
       int oy, ox, on;
       origin(tt, oy, ox, on);
@@ -303,16 +329,45 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
             v[0] += bf16lo(eo[i][jn][0]); v[1] += bf16hi(eo[i][jn][0]);
             v[2] += bf16lo(eo[i][jn][1]); v[3] += bf16hi(eo[i][jn][1]);
           }
+#ifdef DW_DIAG_NO_STORE
+          if (flags & (1 << 30))   // never at run time: the values stay live
+#endif
           *(u32x2*)(ob + ((2 * rw + i) * W + r) * (int)d.out_ps + coff_o[jn]) = rdn_pack4(v);
         }
     };
 
     u32x4 lA[D_IT], gA[D_IT], lB[D_IT], gB[D_IT];
     u32x2 eC[MT][NTL], eN[MT][NTL];
+    if constexpr (Cfg::SB) {
+    // step k computes tile t from buffer k&1 while it gates tile t + per (issued one
+    // step earlier) into buffer (k+1)&1 and issues tile t + 2 per: ONE barrier per
+    // tile, and the gate pass overlaps the W waves' MFMAs instead of idling them (two
+    // register sets in flight measured no faster and spill the 80-column shape)
     if (t < t_hi) {
       load(t, lA, gA);
       load_epi(t, eC);
-      store(lA, gA, true);
+      store(lA, gA, true, 0);
+      load(min(t + per, t_last), lA, gA);
+    }
+    __syncthreads();   // weights + first halos
+    auto step = [&](u32x4 (&lc)[D_IT], u32x4 (&gc)[D_IT], const u32x2 (&ec)[MT][NTL], u32x2 (&en)[MT][NTL],
+                    int cur) -> bool {
+      const int t1 = t + per;
+      store(lc, gc, t1 < t_hi, (cur ^ 1) * Cfg::D_BYTES);   // (past the range: a re-read of the last tile)
+      load(min(t + 2 * per, t_last), lc, gc);
+      load_epi(min(t1, t_last), en);
+      dgrad_tile(t, ec, cur * Cfg::D_BYTES);   // MFMAs + dX stores
+      __syncthreads();   // buffer cur consumed, buffer cur^1 written
+      t = t1;
+      return t < t_hi;
+    };
+    if (t < t_hi)
+      while (step(lA, gA, eC, eN, 0) && step(lA, gA, eN, eC, 1)) {}
+    } else {
+    if (t < t_hi) {
+      load(t, lA, gA);
+      load_epi(t, eC);
+      store(lA, gA, true, 0);
       load(min(t + per, t_last), lA, gA);
     }
     __syncthreads();   // weights + first halos
@@ -321,15 +376,16 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       const int t1 = t + per;
       load(min(t + 2 * per, t_last), ln, gn);
       load_epi(min(t1, t_last), en);
-      dgrad_tile(t, ec);   // MFMAs + dX stores
+      dgrad_tile(t, ec, 0);   // MFMAs + dX stores
       __syncthreads();   // halos of t consumed
-      store(lc, gc, t1 < t_hi);   // unconditional (past the range: a re-read of the last tile)
+      store(lc, gc, t1 < t_hi, 0);   // unconditional (past the range: a re-read of the last tile)
       __syncthreads();   // halos of t1 visible
       t = t1;
       return t < t_hi;
     };
     if (t < t_hi)
       while (step(lA, gA, lB, gB, eC, eN) && step(lB, gB, lA, gA, eN, eC)) {}
+    }
 
     // dalpha / dbias partials of this split into LDS (the loop ended with a barrier
     // that both roles passed, so the halo area is free); summed below
@@ -363,7 +419,11 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       const __amdgpu_buffer_rsrc_t rx = rdn_rsrc(XS + hpix0 * wg.b_ps);
 #pragma unroll
       for (int it = 0; it < X_IT; ++it)
+#ifdef DW_DIAG_NO_LOAD
+        lr[it] = u32x4{(unsigned)in_img(llds[it] < 0 ? HW_ : llds[it] / XROW, oy, ox), 0u, 0u, 0u};
+#else
         lr[it] = rdn_ld16(rx, in_img(llds[it] < 0 ? HW_ : llds[it] / XROW, oy, ox), lrel[it] * 2);
+#endif
     };
     auto store = [&](const u32x4 (&lr)[X_IT], int xoff) {
 #pragma unroll
@@ -386,7 +446,52 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     for (int i = 0; i < MTW; ++i)
 #pragma unroll
       for (int j = 0; j < NTW; ++j) accW[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    auto wgrad_tile = [&](int xoff) {
+#if DW_WPIPE > 0
+    // (k-step, n-tile) steps in one software pipeline: the B fragments of step s + PD
+    // are read before step s's MFMAs, the A fragments of k-step ks + 1 at the start of
+    // ks (the plain per-k-step form waited on each fragment right after reading it:
+    // with MTW = 1-2 MFMAs per fragment the LDS latency was exposed at every step)
+    auto wgrad_tile = [&](int xoff, int doff) {
+      constexpr int PD = DW_WPIPE, NQ = PD + 1, KS = TH / 2, NS = KS * NTW;
+      auto rdA = [&](int ks, bf16x8 (&a)[MTW]) {
+#pragma unroll
+        for (int i = 0; i < MTW; ++i) {
+          const i16x4 lo =
+              __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, pwa + doff + (2 * ks) * RS * DROW + i * 32));
+          const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              RDN_LDS_PTR(i16x4, pwa + doff + (2 * ks + 1) * RS * DROW + i * 32));
+          a[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        }
+      };
+      auto rdB = [&](int st) {   // (an n-tile past NT_ALL reads column 0: uniform, unused)
+        const unsigned char* b = pwb + xoff + boff(st % NTW) + (2 * (st / NTW)) * RS * XROW;
+        const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, b));
+        const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, b + RS * XROW));
+        return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      };
+      bf16x8 af[2][MTW], bq[NQ];
+      rdA(0, af[0]);
+#pragma unroll
+      for (int p = 0; p < PD && p < NS; ++p) bq[p] = rdB(p);
+#pragma unroll
+      for (int st = 0; st < NS; ++st) {
+        const int ks = st / NTW, j = st % NTW;
+        if (j == 0 && ks + 1 < KS) rdA(ks + 1, af[(ks + 1) & 1]);
+        if (st + PD < NS) bq[(st + PD) % NQ] = rdB(st + PD);
+        if (rw + 4 * j < NT_ALL) {   // wave-uniform
+#pragma unroll
+          for (int i = 0; i < MTW; ++i)
+#ifdef DW_DIAG_NO_MFMA
+            accW[i][j][0] += __builtin_bit_cast(float, __builtin_bit_cast(u32x4, af[ks & 1][i])[0] ^
+                                                           __builtin_bit_cast(u32x4, bq[st % NQ])[0]);
+#else
+            accW[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks & 1][i], bq[st % NQ], accW[i][j], 0, 0, 0);
+#endif
+        }
+      }
+    };
+#else
+    auto wgrad_tile = [&](int xoff, int doff) {
 #pragma unroll
       for (int ks = 0; ks < TH / 2; ++ks) {
         __builtin_amdgcn_sched_barrier(0);   // k-steps stay apart: fragment registers of one at a time
@@ -394,9 +499,9 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
 #pragma unroll
         for (int i = 0; i < MTW; ++i) {
           const i16x4 lo =
-              __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, pwa + (2 * ks) * RS * DROW + i * 32));
-          const i16x4 hi =
-              __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, pwa + (2 * ks + 1) * RS * DROW + i * 32));
+              __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, pwa + doff + (2 * ks) * RS * DROW + i * 32));
+          const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              RDN_LDS_PTR(i16x4, pwa + doff + (2 * ks + 1) * RS * DROW + i * 32));
           af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
         }
 #pragma unroll
@@ -408,11 +513,40 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
           const bf16x8 bfr = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
 #pragma unroll
           for (int i = 0; i < MTW; ++i)
+#ifdef DW_DIAG_NO_MFMA
+            accW[i][j][0] += __builtin_bit_cast(float, __builtin_bit_cast(u32x4, af[i])[0] ^ __builtin_bit_cast(u32x4, bfr)[0]);
+#else
             accW[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, accW[i][j], 0, 0, 0);
+#endif
         }
       }
     };
+#endif
 
+    if constexpr (Cfg::SB) {
+    // the D waves' schedule (one barrier per tile): step k computes tile t from X
+    // buffer k&1 (and the dY halo buffer k&1) while tile t + per, issued one step
+    // earlier, goes to buffer (k+1)&1.  One register set for every shape (two, for
+    // the shapes whose budget held them, spilled once both parities were unrolled)
+    // and a run-time parity (unrolled, the two copies spilled the 64 / 80-column ones)
+    {
+      u32x4 lA[X_IT];
+      if (t < t_hi) {
+        load(t, lA);
+        store(lA, 0);
+        load(min(t + per, t_last), lA);
+      }
+      __syncthreads();   // weights + first halos
+      for (int k = 0; t < t_hi; ++k) {
+        const int cur = k & 1;
+        store(lA, (cur ^ 1) * Cfg::X_BYTES);   // tile t + per (a re-read past the range)
+        load(min(t + 2 * per, t_last), lA);
+        wgrad_tile(cur * Cfg::X_BYTES, cur * Cfg::D_BYTES);
+        __syncthreads();   // buffers cur consumed, buffers cur^1 written
+        t += per;
+      }
+    }
+    } else {
     if constexpr (DW2) {   // two tiles in flight: register sets alternate
       u32x4 lA[X_IT], lB[X_IT];
       if (t < t_hi) {
@@ -423,7 +557,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       __syncthreads();   // weights + first halos
       auto step = [&](u32x4 (&lc)[X_IT], u32x4 (&ln)[X_IT]) -> bool {
         load(min(t + 2 * per, t_last), ln);
-        wgrad_tile(0);
+        wgrad_tile(0, 0);
         __syncthreads();   // halos of t consumed
         store(lc, 0);
         __syncthreads();   // halos of t1 visible
@@ -447,7 +581,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       while (t < t_hi) {
         store(lA, ((k + 1) & 1) * Cfg::X_BYTES);   // tile t + per (a re-read past the range)
         load(min(t + 2 * per, t_last), lA);
-        wgrad_tile((k & 1) * Cfg::X_BYTES);
+        wgrad_tile((k & 1) * Cfg::X_BYTES, 0);
         __syncthreads();   // halos of t consumed; X of t + per visible
         __syncthreads();   // (the D waves' dY halo of t + per)
         t += per;
@@ -462,12 +596,14 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       __syncthreads();   // weights + first halos
       while (t < t_hi) {
         load(min(t + per, t_last), lA);
-        wgrad_tile(0);
+        wgrad_tile(0, 0);
         __syncthreads();   // halos of t consumed
         store(lA, 0);
         __syncthreads();   // halos of t1 visible
         t += per;
       }
+    }
+
     }
 
     // this block's split of the weight gradient (zero slab for a block without tiles)
