@@ -340,6 +340,14 @@ def metrics_bench(dev, n=64, size=256):
             "note": "per-block skimage on the host (reference) is not timed here"}
 
 
+class GraphCaptureError(RuntimeError):
+    """The hipGraph capture of a data-parallel step raised; `trainer` is usable eagerly."""
+
+    def __init__(self, trainer):
+        super().__init__("graph capture of the data-parallel train step failed")
+        self.trainer = trainer
+
+
 class Trainer:
     """One RDUNet_T train step (the timed unit) for a (per-GPU batch, dtype):
     synthetic seeded data resident in HBM, FusedAdamW every step."""
@@ -371,7 +379,13 @@ class Trainer:
         self.graph = None
         if graph:   # the whole step as one hipGraph replay (train_graph.TrainStepGraph)
             from vub_image_denoising_amd.train_graph import TrainStepGraph
-            self.graph = TrainStepGraph(self.model, self.opt, tuple(self.batches[0][0].shape), 'uniform', 1.0)
+            try:
+                self.graph = TrainStepGraph(self.model, self.opt, tuple(self.batches[0][0].shape), 'uniform', 1.0)
+            except Exception as e:
+                if world == 1:
+                    raise
+                self.graph = None
+                raise GraphCaptureError(self) from e
 
     def step(self, i):
         noisy, clean = self.batches[i % 3]
@@ -457,6 +471,65 @@ def dense_conv_path(prof, batch):
             "note": "isolated (serialised-backward) launch times; bytes incl. the fused PReLU-backward gate reads"}
 
 
+# a rank whose hipGraph capture of the data-parallel step raised exits with this code;
+# the launcher then starts the whole job again, eagerly (--graph off), in fresh processes
+EXIT_GRAPH_FAILED = 3
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _run_ranks(n, argv, grace_s=60.0):
+    """Start n ranks of this bench (fresh child processes, one per GPU: RANK /
+    LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment, rendezvous on
+    127.0.0.1) and wait for them.  When a rank fails the others get `grace_s` to
+    finish before their process groups are killed (a rank left waiting in a
+    collective would never return).  Returns the ranks' exit codes."""
+    import signal
+    import subprocess
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RDN_BENCH_LAUNCHED="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env,
+                                      start_new_session=True))
+    failed_at = None
+    while True:
+        rcs = [p.poll() for p in procs]
+        if all(rc is not None for rc in rcs):
+            return rcs
+        if failed_at is None and any(rc not in (None, 0) for rc in rcs):
+            failed_at = time.monotonic()
+        if failed_at is not None and time.monotonic() - failed_at > grace_s:
+            for p in procs:
+                if p.poll() is None:
+                    os.killpg(p.pid, signal.SIGKILL)
+            return [p.wait() for p in procs]
+        time.sleep(0.2)
+
+
+def launch(args, argv):
+    """`--gpus N` (N > 1) without a launcher's environment: run the N ranks as child
+    processes of this one -- which never touches the GPU itself -- so that
+    `python bench.py --gpus N` measures N GPUs exactly as
+    `torchrun --nproc-per-node N bench.py --gpus N` does.  If a rank reports that
+    the hipGraph capture of the RCCL step raised (exit EXIT_GRAPH_FAILED), the job
+    runs again from fresh processes with --graph off."""
+    rcs = _run_ranks(args.gpus, argv)
+    if EXIT_GRAPH_FAILED in rcs and args.graph == "on":
+        _log(f"graph capture failed on a rank (exit codes {rcs}); running the job again eagerly (--graph off)")
+        rcs = _run_ranks(args.gpus, [*argv, "--graph", "off"])
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -475,18 +548,56 @@ def main():
     ap.add_argument("--graph", choices=["on", "off"], default="on",
                     help="time the step as one hipGraph replay (train_graph.TrainStepGraph) or eagerly")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--launch-dry-run", action="store_true",
+                    help="ranks report RANK/LOCAL_RANK/WORLD_SIZE as JSON and exit before touching the GPU")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend for N > 1 (nccl = RCCL; gloo only for eager plumbing tests)")
+    ap.add_argument("--one-device", action="store_true",
+                    help="every rank on cuda:0 (plumbing tests of N > 1 on a 1-GPU box; gloo, --graph off)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch(args, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a {world}-rank run as "
+              f"{args.gpus} GPUs", file=sys.stderr)
+        sys.exit(2)
+    if args.launch_dry_run:
+        if os.environ.get("RDN_BENCH_DRY_GRAPH_FAIL") and args.graph == "on":   # tests of the eager restart
+            sys.exit(EXIT_GRAPH_FAILED)
+        print(json.dumps({"rank": rank, "local_rank": local, "world_size": world, "graph": args.graph,
+                          "master_addr": os.environ.get("MASTER_ADDR"), "master_port": os.environ.get("MASTER_PORT"),
+                          "launched_by": "bench.py" if os.environ.get("RDN_BENCH_LAUNCHED") else "external"}),
+              flush=True)
+        return
+    if args.one_device:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     graph = args.graph == "on" and not args.pmc_child
-    tr = Trainer(dev, args.batch, args.size, args.base_filters, args.dtype, rank, world, graph=graph)
+    try:
+        tr = Trainer(dev, args.batch, args.size, args.base_filters, args.dtype, rank, world, graph=graph)
+    except GraphCaptureError as e:
+        # the hipGraph capture of the data-parallel step raised: under this bench's own
+        # launcher the job restarts eagerly from fresh processes; under an external
+        # launcher (torchrun) this rank continues eagerly in-process
+        _log(f"rank {rank}: graph capture failed ({e.__cause__!r})")
+        if os.environ.get("RDN_BENCH_LAUNCHED"):
+            if world > 1:
+                dist.destroy_process_group()
+            sys.exit(EXIT_GRAPH_FAILED)
+        graph = False
+        tr = e.trainer
+    graph = tr.graph is not None
     for i in range(args.warmup):
         tr.step(i)
     torch.cuda.synchronize()
@@ -567,10 +678,10 @@ def main():
             torch.cuda.empty_cache()
             extra = extra_configs(dev, args)
             roof["dense_conv_path"] = extra["b32"].pop("dense_conv_path")
-        if not (args.no_cpu_baseline or args.pmc_child):
+        want_cpu = world == 1 and not (args.no_cpu_baseline or args.pmc_child)   # rank 0 at N = 1 only
+        if want_cpu:
             _log("CPU baseline")
-        cpu = None if (args.no_cpu_baseline or args.pmc_child) else cpu_baseline(args.cpu_seconds, args.batch,
-                                                                                 args.size)
+        cpu = cpu_baseline(args.cpu_seconds, args.batch, args.size) if want_cpu else None
         infer = None
         if not (args.no_inference or args.pmc_child) and world == 1:
             _log("sampler measurements")
@@ -599,6 +710,10 @@ def main():
                        "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                        "image": [3, args.size, args.size], "timesteps": 20,
                        "parallelism": f"dp{world}", "optimizer_step": "every step",
+                       "launcher": ("single process" if world == 1 else
+                                    "bench.py child processes" if os.environ.get("RDN_BENCH_LAUNCHED") else
+                                    "external (torchrun)"),
+                       "dist_backend": (args.dist_backend if world > 1 else None),
                        "final_loss": round(loss_v, 5)},
             "b32_images_per_s": extra["b32"]["images_per_s"] if extra else None,
             "fp32_images_per_s": extra["fp32"]["images_per_s"] if extra else None,

@@ -259,6 +259,12 @@ int rdn_charbonnier_bwd(const float* pred, const float* target, int64_t count, f
 
 /* out[0] = sqrt(sum g^2) over a flat fp32 buffer; out[1] = min(max_norm/(out[0]+1e-6), 1) */
 int rdn_sqnorm(const float* g, int64_t count, float max_norm, float* ws, float* out, void* stream);
+/* the same for pre_scale*g without scaling g (pre_scale > 0: the data-parallel 1/world
+ * average folded into the clip): out[0] = norm of pre_scale*g, out[1] = pre_scale *
+ * min(max_norm/(out[0]+1e-6), 1); rdn_clip_scale with out+1 then leaves the averaged,
+ * clipped gradient.  Bit-identical to averaging first when pre_scale is a power of two. */
+int rdn_sqnorm_scaled(const float* g, int64_t count, float max_norm, float pre_scale, float* ws, float* out,
+                      void* stream);
 /* g *= coef[0] (device scalar; no host sync) */
 int rdn_clip_scale(float* g, int64_t count, const float* coef, void* stream);
 

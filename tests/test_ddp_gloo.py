@@ -45,13 +45,14 @@ def test_plan_buckets_cover_everything_once():
     assert any(hi - lo >= 900000 for lo, hi in covered)
 
 
-def _worker(rank, world, init_file, q):
+def _worker(rank, world, init_file, q, defer=False):
     # file:// rendezvous: no TCP port to race for between parallel test runs
     dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
     try:
         fp = _fake_flat(100 + rank, SIZES)
         mine = fp.gflat.clone()
         gs = GradSync(fp, bucket_mb=0.4, overlap=False)
+        gs.defer_average = defer
         gs.begin()
         # backward order: parameters complete from the last to the first, in groups of 3
         idx = list(range(len(SIZES)))[::-1]
@@ -59,6 +60,9 @@ def _worker(rank, world, init_file, q):
             gs.params_done(idx[i:i + 3])
         assert all(gs._launched), "every bucket launched once its parameters completed"
         gs.finish()
+        if defer:   # the sum is left in place and the 1/world factor handed to the caller
+            assert gs.take_pending() == 1.0 / world and gs.take_pending() is None
+            fp.gflat.mul_(1.0 / world)
         # numpy arrays travel by value; a torch tensor would be shared through a
         # file descriptor whose socket dies with this process (racy FileNotFoundError)
         q.put((rank, mine.numpy(), fp.gflat.clone().numpy()))
@@ -74,11 +78,12 @@ def _free_port():
     return p
 
 
-def test_gradsync_world2_gloo_average(tmp_path):
+@pytest.mark.parametrize("defer", [False, True], ids=["average", "deferred"])
+def test_gradsync_world2_gloo_average(tmp_path, defer):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     init_file = str(tmp_path / "rendezvous")
-    procs = [ctx.Process(target=_worker, args=(r, 2, init_file, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, init_file, q, defer)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict()

@@ -108,6 +108,26 @@ def test_two_forwards_before_backward():
         assert torch.equal(p.grad, a + b)
 
 
+def test_many_forwards_before_one_backward():
+    """Six same-shape grad-enabled forwards alive at once, then ONE backward of the
+    summed loss (micro-batches summed before backward, as autograd allows): each
+    forward holds its own pooled engine (activations), the pool's backward scratch is
+    shared, and every gradient equals the sum of the per-batch gradients."""
+    from vub_image_denoising_amd import engine as E
+    m = _net()
+    params = list(m.parameters())
+    data = [_data(seed=10 + i) for i in range(6)]
+    refs = [torch.autograd.grad(_loss(m, x, t), params) for x, t in data]
+    total = sum(_loss(m, x, t) for x, t in data)
+    pool = [v for k, v in m._rdn_engines.items() if k[-1]][0]
+    assert len(pool) >= 6 and len({id(e.scratch) for e in pool}) == 1
+    total.backward()
+    for i, p in enumerate(params):
+        want = sum(r[i] for r in refs)
+        assert torch.allclose(p.grad, want, rtol=1e-5, atol=1e-7), m._rdn_flat.names[i]
+    assert E.MAX_TRAIN_ENGINES == 0 or E.MAX_TRAIN_ENGINES >= 6
+
+
 def test_retain_graph_and_release():
     m = _net()
     x, t = _data()

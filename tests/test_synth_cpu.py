@@ -131,3 +131,23 @@ def test_cpu_load_sidd_data(tmp_path):
     assert torch.equal(gt, torch.from_numpy(S.to_unit(gts[scenes[0]][:256, 256:512])))
     tr, va = load_sidd_data(str(root), batch_size=2, num_workers=0, validation_split=0.5, use_rgb=True)
     assert len(tr.dataset) == 2 and len(va.dataset) == 2
+
+
+def test_mixed_patch_loader_alternates():
+    """Config 5's stream: batches taken from each patch-size loader in turn until all
+    are exhausted (synth.MixedPatchLoader)."""
+    from vub_image_denoising_amd.synth import MixedPatchLoader
+
+    class L:
+        def __init__(self, tag, n):
+            self.tag, self.n, self.batch_size, self.dataset = tag, n, 2, list(range(2 * n))
+
+        def __len__(self):
+            return self.n
+
+        def __iter__(self):
+            return iter([(self.tag, i) for i in range(self.n)])
+
+    m = MixedPatchLoader([L(128, 3), L(256, 1)])
+    assert len(m) == 4 and len(m.dataset) == 8
+    assert list(m) == [(128, 0), (256, 0), (128, 1), (128, 2)]

@@ -104,6 +104,7 @@ SIGNATURES = {
     "rdn_charbonnier_fwd": (_i32, [_vp, _vp, _i64, _f32, _vp, _vp, _vp]),
     "rdn_charbonnier_bwd": (_i32, [_vp, _vp, _i64, _f32, _f32, _f32, _vp, _vp, _vp]),
     "rdn_sqnorm": (_i32, [_vp, _i64, _f32, _vp, _vp, _vp]),
+    "rdn_sqnorm_scaled": (_i32, [_vp, _i64, _f32, _f32, _vp, _vp, _vp]),
     "rdn_clip_scale": (_i32, [_vp, _i64, _vp, _vp]),
     "rdn_adam_step": (_i32, [_vp, _vp, _vp, _vp, _i64, C.c_double, C.c_double, C.c_double, C.c_double, C.c_double,
                              _i32, _i64, _vp, _f32, _vp]),

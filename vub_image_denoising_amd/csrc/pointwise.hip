@@ -377,8 +377,11 @@ __global__ __launch_bounds__(256) void sq_partial_kernel(const float* __restrict
   if (threadIdx.x == 0) part[blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
 }
 
+// pre: a scale the caller has not applied to g yet (the data-parallel 1/world average,
+// ddp.GradSync.defer_average): the norm is that of pre*g and out[1] carries pre; for a
+// power-of-two pre both are exactly what scaling g first would give
 __global__ __launch_bounds__(256) void sq_final_kernel(const float* __restrict__ part, int nb, float max_norm,
-                                                       float* __restrict__ out) {
+                                                       float pre, float* __restrict__ out) {
   double s = 0.0;
   for (int i = threadIdx.x; i < nb; i += 256) s += part[i];
   __shared__ double sh[256];
@@ -389,10 +392,10 @@ __global__ __launch_bounds__(256) void sq_final_kernel(const float* __restrict__
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    const float tot = (float)sqrt(sh[0]);
+    const float tot = (float)(sqrt(sh[0]) * (double)pre);
     out[0] = tot;
     const float coef = max_norm / (tot + 1e-6f);
-    out[1] = coef < 1.f ? coef : 1.f;
+    out[1] = pre * (coef < 1.f ? coef : 1.f);
   }
 }
 
@@ -620,12 +623,20 @@ extern "C" int rdn_charbonnier_bwd(const float* pred, const float* target, int64
   return rdn_check_launch("rdn_charbonnier_bwd");
 }
 
-extern "C" int rdn_sqnorm(const float* g, int64_t count, float max_norm, float* ws, float* out, void* stream) {
-  if (!g || !ws || !out || count <= 0 || ((uintptr_t)g & 15)) { rdn_set_error("rdn_sqnorm: bad arguments"); return RDN_E_ARG; }
+extern "C" int rdn_sqnorm_scaled(const float* g, int64_t count, float max_norm, float pre_scale, float* ws, float* out,
+                                 void* stream) {
+  if (!g || !ws || !out || count <= 0 || ((uintptr_t)g & 15) || !(pre_scale > 0.f)) {
+    rdn_set_error("rdn_sqnorm: bad arguments");
+    return RDN_E_ARG;
+  }
   const int nb = grid_for(count, 256 * 16, kRedBlocks);
   sq_partial_kernel<<<nb, 256, 0, RDN_STREAM>>>(g, count, ws);
-  sq_final_kernel<<<1, 256, 0, RDN_STREAM>>>(ws, nb, max_norm, out);
+  sq_final_kernel<<<1, 256, 0, RDN_STREAM>>>(ws, nb, max_norm, pre_scale, out);
   return rdn_check_launch("rdn_sqnorm");
+}
+
+extern "C" int rdn_sqnorm(const float* g, int64_t count, float max_norm, float* ws, float* out, void* stream) {
+  return rdn_sqnorm_scaled(g, count, max_norm, 1.f, ws, out, stream);
 }
 
 extern "C" int rdn_clip_scale(float* g, int64_t count, const float* coef, void* stream) {

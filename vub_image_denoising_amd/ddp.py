@@ -19,8 +19,11 @@ Design for MI355X (xGMI point-to-point mesh):
   backward has finished the last layer whose gradients it holds, so RCCL rings
   run on the links while the remaining layers' dgrad/wgrad run on the compute
   stream;
-* the 1/world average is folded into one in-place scale after the last
-  bucket (so clip_grad_norm_ sees the mean gradient, as torch DDP would).
+* the 1/world average is one in-place scale after the last bucket (so
+  clip_grad_norm_ sees the mean gradient, as torch DDP would) -- or, when the
+  caller clips right after the backward (``defer_average``, set by
+  train_step_device), it is folded into the clip's own scale pass
+  (rdn_sqnorm_scaled): one pass over the 41.6 MB gradient instead of two.
 
 No wrapper around the model: ``train_step_checkpointed`` calls
 ``model.unet(...)`` directly (diffusion_RDUnet.py:106), which would bypass a DDP
@@ -79,12 +82,17 @@ class GradSync:
         self._srcs = [[] for _ in self.buckets]
         self._inv = None
         self.buf = fp.gflat
+        # defer_average: finish() leaves the sum and records the 1/world factor in
+        # `pending` for the caller's clip (take_pending) instead of scaling
+        self.defer_average = False
+        self.pending = None
 
     # --- engine hooks -------------------------------------------------
     def begin(self, buf=None):
         """A backward starts producing its gradients into ``buf`` (a flat
         buffer of ``fp``'s layout; default ``fp.gflat``)."""
         self.buf = self.fp.gflat if buf is None else buf
+        self.pending = None
         self._works = []
         self._remaining = list(self.counts)
         self._launched = [False] * len(self.buckets)
@@ -137,7 +145,16 @@ class GradSync:
             torch.cuda.current_stream().wait_stream(self.stream)
         self._works = []
         if self.world > 1:
-            self._average()
+            if self.defer_average:
+                self.pending = 1.0 / self.world
+            else:
+                self._average()
+
+    def take_pending(self):
+        """The 1/world factor a deferred finish() left unapplied (None if none);
+        the caller applies it (clip_grad_norm_flat's pre_scale)."""
+        p, self.pending = self.pending, None
+        return p
 
     def _average(self):
         g = self.buf

@@ -103,9 +103,29 @@ def train_step_device(model, clean_images, noisy_images, optimizer, distribution
     if zero_grad:
         optimizer.zero_grad()
     loss = _forward_loss(model, clean_images, noisy_images, distribution_choice, t)
-    loss.backward()                                                                    # :110
+    # data-parallel: the clip right after the backward also applies the 1/world
+    # average of the all-reduced gradient (one pass instead of two, ddp.py)
+    fp = getattr(model.unet, "_rdn_flat", None)
+    sync = getattr(fp, "grad_sync", None) if clip else None
+    fold = sync is not None and sync.world > 1
+    if fold:
+        sync.defer_average = True
+    try:
+        loss.backward()                                                                # :110
+    finally:
+        if fold:
+            sync.defer_average = False
     if clip:
-        Fn.clip_grad_norm_(model.parameters(), clip_value)                             # :113
+        pre = sync.take_pending() if fold else None
+        params = list(model.parameters())
+        flat = Fn.find_flat(params) if pre is not None else None
+        if pre is not None and flat is None:
+            sync._average()   # gradients not the flat views: average them first
+            pre = None
+        if pre is not None:
+            Fn.clip_grad_norm_flat(flat, clip_value, pre_scale=pre)                    # :113
+        else:
+            Fn.clip_grad_norm_(params, clip_value)                                     # :113
     return loss
 
 

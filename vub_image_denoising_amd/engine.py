@@ -545,7 +545,8 @@ class UNetEngine:
     """Buffers and prebuilt launch descriptors of one Program (the network, or
     one block) for one input shape (B, H, W of level 0)."""
 
-    def __init__(self, module, B, Hh, Ww, dtype, train: bool, prog: Program | None = None, params=None):
+    def __init__(self, module, B, Hh, Ww, dtype, train: bool, prog: Program | None = None, params=None,
+                 scratch: dict | None = None):
         if prog is None:
             F0 = module.base_filters
             if F0 % 16:
@@ -555,6 +556,12 @@ class UNetEngine:
             raise RuntimeError(f"{type(module).__name__} needs H and W divisible by {prog.min_div}; got {Hh}x{Ww}")
         self.module = module
         self.prog = prog
+        # backward-only buffers (activation gradients, dYpre / partial / slab slots,
+        # workspaces), shared by every grad-enabled engine of one (shape, dtype) pool:
+        # backwards run one after another on the compute stream (each ends by waiting
+        # for its weight-gradient stream), so one set serves all of them and a pooled
+        # engine costs only its forward activations and PReLU inputs
+        self.scratch = {} if scratch is None else scratch
         self.B, self.H, self.W = B, Hh, Ww
         self.dtype = dtype
         self.code = H.dtype_code(dtype)
@@ -576,16 +583,20 @@ class UNetEngine:
         # gradients are only computed when that input needs a gradient
         self.pure_inputs = in_bufs - {L.dst.buf for L in layers if L.dst is not None}
 
-        def alloc(name, lvl, ch):
+        def alloc(name, lvl, ch, shared=False):
             cb = prog.cb.get(lvl, 0)
             if (PLANAR and cb and name not in in_bufs and name[1:] not in in_bufs and not name.startswith("PRE_")
                     and ch % cb == 0 and ch > cb):
                 pl = self.P[lvl] * cb
-                t = torch.zeros(ch // cb, pl, dtype=dtype, device=dev)
+                shape = (ch // cb, pl)
                 self.geo[name] = (cb, pl)
             else:
-                t = torch.zeros(self.P[lvl], ch, dtype=dtype, device=dev)
+                shape = (self.P[lvl], ch)
                 self.geo[name] = (ch, 0)
+            if shared:
+                t = self._shared(("buf", name), lambda: torch.zeros(shape, dtype=dtype, device=dev))
+            else:
+                t = torch.zeros(shape, dtype=dtype, device=dev)
             self.bufs[name] = t
 
         for name, (lvl, ch) in bufspec.items():
@@ -599,7 +610,7 @@ class UNetEngine:
             for name, (lvl, ch) in bufspec.items():
                 if name.startswith("PRE_"):
                     continue
-                alloc("d" + name, lvl, ch)
+                alloc("d" + name, lvl, ch, shared=True)
             # weight gradients (wgrad + reduce) run on a side stream, overlapped with
             # the dgrad chain; the dYpre / PReLU-partial / slab buffers they read live in
             # SLOTS slots (layer b of the backward order uses slot b % SLOTS), each sized
@@ -613,13 +624,21 @@ class UNetEngine:
             sizes = [0] * self.slots
             for b, L in enumerate(reversed(layers)):
                 sizes[b % self.slots] = max(sizes[b % self.slots], self.P[self._out_level(L)] * L.cout_pad)
-            self.dyp = [torch.zeros(n, dtype=dtype, device=dev) for n in sizes]
+            self.dyp = [self._shared(("dyp", i), lambda n=n: torch.zeros(n, dtype=dtype, device=dev))
+                        for i, n in enumerate(sizes)]
             self._build_bwd()
         self._build_info()
         self.lease = None   # weakref to the autograd graph's lease while it owns the activations
         self.lease_seq = 0
 
     # ------------------------------------------------------------------
+    def _shared(self, key, make):
+        """A backward scratch buffer of this engine's pool (made on first use)."""
+        t = self.scratch.get(key)
+        if t is None:
+            t = self.scratch[key] = make()
+        return t
+
     def _out_level(self, L):
         return L.level - 1 if L.kind == "up" else L.level
 
@@ -833,7 +852,8 @@ class UNetEngine:
             L.extra["goff"] = [4 * self.fp.offsets[i] for i in pidx]   # byte offsets in a flat gradient buffer
             L.extra["olvl"] = olvl
         self._plan_gate_out()
-        self.ws = torch.zeros(max(ws_need // 4, 4), dtype=torch.float32, device=self.device)
+        self.ws = self._shared("ws", lambda: torch.zeros(max(ws_need // 4, 4), dtype=torch.float32,
+                                                          device=self.device))
         # per slot: fused layers' slabs (written from the compute stream while the side
         # stream may still reduce an earlier layer's) and the dalpha/dbias partials
         dwb, pwb = [0] * self.slots, [16] * self.slots
@@ -842,8 +862,10 @@ class UNetEngine:
             dwb[sl] = max(dwb[sl], L.extra["dw_bytes"])
             pwb[sl] = max(pwb[sl], L.extra["part_bytes"])
         f32 = dict(dtype=torch.float32, device=self.device)
-        self.ws_dw = [torch.zeros((n // 4 + 3) // 4 * 4, **f32) if n else None for n in dwb]
-        self.pws = [torch.zeros((n // 4 + 3) // 4 * 4, **f32) for n in pwb]
+        self.ws_dw = [self._shared(("ws_dw", i), lambda n=n: torch.zeros((n // 4 + 3) // 4 * 4, **f32)) if n else None
+                      for i, n in enumerate(dwb)]
+        self.pws = [self._shared(("pws", i), lambda n=n: torch.zeros((n // 4 + 3) // 4 * 4, **f32))
+                    for i, n in enumerate(pwb)]
         for L in self.layers:
             L.extra["pws"] = self.pws[L.extra["slot"]].data_ptr()
             L.wgrad_desc.ws = self.ws_dw[L.extra["slot"]].data_ptr() if L.extra["dw"] else self.ws.data_ptr()
@@ -860,17 +882,17 @@ class UNetEngine:
             self.ev_begin = torch.cuda.Event()
             self.ev_end = torch.cuda.Event()
 
-    def _plan_gate_out(self) -> int:
+    def _plan_gate_out(self) -> None:
         """Pair every layer that still needs a separate PReLU-backward pass with the
         last consumer of its output in backward order when that consumer's input
         gradient has the layer's output as the tail of its columns (dense conv_k+1
         for slice out_k, Unet_model.py:81-87; up_l.conv for up_l.conv_t's output,
         :43), and let that epilogue write the layer's dYpre and dalpha/dbias
-        partials (rdn_conv_desc.gout).  Returns the partial-workspace bytes needed."""
+        partials (rdn_conv_desc.gout).  The partials' bytes go into the gated layer's
+        ``part_bytes`` (sized into its slot's pws buffer)."""
         if not GATE_OUT:
-            return 0
+            return
         lib = H.lib()
-        need = 0
         index = {id(L): i for i, L in enumerate(self.layers)}
         for K in self.layers:
             # (level 0: the finisher's 8-byte-per-lane epilogue streams the extra PReLU
@@ -906,8 +928,6 @@ class UNetEngine:
             K.extra["gated_by"] = J
             K.extra["part_rows"] = rows
             K.extra["part_bytes"] = max(K.extra["part_bytes"], rows * 2 * K.cout * 4)
-            need = max(need, rows * 2 * K.cout * 4)
-        return need
 
     @staticmethod
     def _probe_copy(desc, cls, keep):
@@ -1184,8 +1204,11 @@ def _engine_free(eng) -> bool:
     return eng.lease is None or eng.lease() is None
 
 
-# full-activation engines per (shape, dtype) that grad-enabled forwards may hold at once
-MAX_TRAIN_ENGINES = 4
+# engines per (shape, dtype) that grad-enabled forwards may hold at once (each holds
+# its forward activations and PReLU inputs; the backward scratch is one per pool).
+# Past the cap the least recently leased engine is taken over, and backward through
+# the graph that held it raises (RDN_MAX_TRAIN_ENGINES; 0 = no cap)
+MAX_TRAIN_ENGINES = int(os.environ.get("RDN_MAX_TRAIN_ENGINES", "16"))
 _LEASE_SEQ = [0]
 _WARNED_POOL: list = []
 
@@ -1221,7 +1244,7 @@ def _run(module, key_shape, xs, t, params, make_engine):
     pool = module._rdn_engines.setdefault(key, [])
     if not need_grad:
         if not pool:
-            pool.append(make_engine(False))
+            pool.append(make_engine(False, None))
         with torch.no_grad():
             return pool[0].forward(xs, t)
     # a graph owns its engine's activations until its backward (or until it is
@@ -1230,16 +1253,17 @@ def _run(module, key_shape, xs, t, params, make_engine):
     # taken over and the graph that held it raises if it is ever backwarded
     eng = next((e for e in pool if _engine_free(e)), None)
     if eng is None:
-        if len(pool) < MAX_TRAIN_ENGINES:
-            eng = make_engine(True)
+        if MAX_TRAIN_ENGINES <= 0 or len(pool) < MAX_TRAIN_ENGINES:
+            eng = make_engine(True, pool[0].scratch if pool else None)
             pool.append(eng)
         else:
             eng = min(pool, key=lambda e: e.lease_seq)
             if not _WARNED_POOL:
                 _WARNED_POOL.append(True)
                 warnings.warn(f"{type(module).__name__}: {MAX_TRAIN_ENGINES} grad-enabled forwards of one shape are "
-                              "alive without a backward; reusing the oldest one's saved activations (its backward "
-                              "will raise). Run evaluation under torch.no_grad().", RuntimeWarning, stacklevel=3)
+                              "alive without a backward; reusing the oldest one's saved activations, so a backward "
+                              "through that forward will raise (raise the cap with RDN_MAX_TRAIN_ENGINES, or run "
+                              "evaluation under torch.no_grad()).", RuntimeWarning, stacklevel=3)
     lease = _Lease()
     eng.lease = weakref.ref(lease)
     _LEASE_SEQ[0] += 1
@@ -1264,7 +1288,7 @@ def run_unet(module, x: torch.Tensor, t: torch.Tensor | None) -> torch.Tensor:
     fp = flat_params(module, x.device)
     B, Hh, Ww = x.size(0), x.size(2), x.size(3)
     return _run(module, (B, Hh, Ww), [x], t, fp,
-                lambda train: UNetEngine(module, B, Hh, Ww, module.compute_dtype, train))
+                lambda train, scratch: UNetEngine(module, B, Hh, Ww, module.compute_dtype, train, scratch=scratch))
 
 
 def run_block(block, xs) -> torch.Tensor:
@@ -1278,5 +1302,5 @@ def run_block(block, xs) -> torch.Tensor:
     lvl0 = prog.inputs[0][1]
     B, Hh, Ww = xs[0].size(0), xs[0].size(2) << lvl0, xs[0].size(3) << lvl0
     return _run(block, (B, Hh, Ww), xs, None, bp,
-                lambda train: UNetEngine(block, B, Hh, Ww, block.compute_dtype, train,
-                                         prog=block_program(block), params=bp))
+                lambda train, scratch: UNetEngine(block, B, Hh, Ww, block.compute_dtype, train,
+                                                  prog=block_program(block), params=bp, scratch=scratch))

@@ -107,10 +107,12 @@ def combined_loss(pred, target, mse_weight=0, charbonnier_weight=1, ssim_weight=
     return loss
 
 
-def clip_grad_norm_flat(fp: FlatParams, max_norm: float) -> torch.Tensor:
+def clip_grad_norm_flat(fp: FlatParams, max_norm: float, pre_scale: float = 1.0) -> torch.Tensor:
     """Global L2 norm of the flat gradient and in-place scale by
     min(max_norm/(norm+1e-6), 1) — torch.nn.utils.clip_grad_norm_ semantics,
-    without a host synchronisation.  Returns the (device) total norm."""
+    without a host synchronisation.  Returns the (device) total norm.
+    ``pre_scale``: a factor not yet applied to the gradient (the data-parallel
+    1/world average, ddp.GradSync.defer_average), folded into the same scale pass."""
     lib = H.lib()
     ws = getattr(fp, "_clip_ws", None)
     if ws is None:
@@ -118,8 +120,8 @@ def clip_grad_norm_flat(fp: FlatParams, max_norm: float) -> torch.Tensor:
                                        device=fp.device)
         fp._clip_out = torch.empty(2, dtype=torch.float32, device=fp.device)
     st = H.stream_ptr()
-    H.check(lib.rdn_sqnorm(fp.gflat.data_ptr(), fp.numel, float(max_norm), ws.data_ptr(), fp._clip_out.data_ptr(),
-                           st), "sqnorm")
+    H.check(lib.rdn_sqnorm_scaled(fp.gflat.data_ptr(), fp.numel, float(max_norm), float(pre_scale), ws.data_ptr(),
+                                  fp._clip_out.data_ptr(), st), "sqnorm")
     H.check(lib.rdn_clip_scale(fp.gflat.data_ptr(), fp.numel, fp._clip_out[1:].data_ptr(), st), "clip_scale")
     return fp._clip_out[0].clone()
 

@@ -202,6 +202,49 @@ class GpuLoader:
                 yield noisy, clean
 
 
+class MixedPatchLoader:
+    """Config 5's mixed patch stream (BASELINE.json: SIDD at 128 and 256; the
+    reference hard-codes 256, SIDD_dataset.py:56,63-66): one loader per patch size
+    (each over its own PatchPool of the same images), batches taken from them in
+    turn -- loader 0, 1, 0, 1, ... -- until every loader is exhausted.  The network
+    takes any H, W divisible by 8; each shape gets its own engine (and, under
+    train_graph.TrainStepGraphs, its own captured step)."""
+
+    def __init__(self, loaders):
+        if not loaders:
+            raise ValueError("MixedPatchLoader: no loaders")
+        self.loaders = list(loaders)
+        self.dataset = [i for ld in self.loaders for i in ld.dataset]
+        self.batch_size = self.loaders[0].batch_size
+
+    def __len__(self):
+        return sum(len(ld) for ld in self.loaders)
+
+    def __iter__(self):
+        its = [iter(ld) for ld in self.loaders]
+        live = list(range(len(its)))
+        while live:
+            for k in list(live):
+                try:
+                    yield next(its[k])
+                except StopIteration:
+                    live.remove(k)
+
+
+def _sizes(patch_size):
+    return [int(patch_size)] if isinstance(patch_size, (int, np.integer)) else [int(p) for p in patch_size]
+
+
+def _mixed(make, patch_size):
+    """(train, val) loaders of one patch size, or MixedPatchLoaders over several."""
+    pairs = [make(ps) for ps in _sizes(patch_size)]
+    if len(pairs) == 1:
+        return pairs[0]
+    tr = [a for a, _ in pairs]
+    va = [b for _, b in pairs]
+    return (None if tr[0] is None else MixedPatchLoader(tr)), MixedPatchLoader(va)
+
+
 def _split(total, dataset_percentage, validation_split, generator):
     """data_loader.py:63-74: optional random subset, then the train/val random_split."""
     idx = list(range(total))
@@ -216,8 +259,20 @@ def _split(total, dataset_percentage, validation_split, generator):
 
 def load_data_gpu(image_folder, batch_size=4, validation_split=0.2, augment=False, dataset_percentage=1.0,
                   only_validation=False, include_noise_level=False, train_noise_levels=None, val_noise_levels=None,
-                  use_rgb=False, patch_size=256, seed=0, device="cuda", pool=None):
-    """``data_loader.load_data`` (data_loader.py:7-79) with device-side synthesis."""
+                  use_rgb=False, patch_size=256, seed=0, device="cuda", pool=None, images=None):
+    """``data_loader.load_data`` (data_loader.py:7-79) with device-side synthesis.
+    ``patch_size`` may be a sequence (e.g. (128, 256)): one pool per size over the
+    same images, batches alternating between them (MixedPatchLoader).  ``images``:
+    uint8 HWC arrays instead of reading ``image_folder``."""
+    if pool is None and (images is not None or not isinstance(patch_size, (int, np.integer))):
+        if images is None:
+            exts = ("png", "jpg", "jpeg")
+            images = [_read_image(os.path.join(image_folder, f), use_rgb) for f in sorted(os.listdir(image_folder))
+                      if f.lower().endswith(exts)]
+        return _mixed(lambda ps: load_data_gpu(image_folder, batch_size, validation_split, augment, dataset_percentage,
+                                               only_validation, include_noise_level, train_noise_levels,
+                                               val_noise_levels, use_rgb, ps, seed, device,
+                                               pool=PatchPool(images, ps, device)), patch_size)
     pool = pool or PatchPool.from_folder(image_folder, use_rgb, patch_size, device)
     if only_validation:
         levels = val_noise_levels if val_noise_levels is not None else [15, 25, 50]
@@ -234,7 +289,16 @@ def load_data_gpu(image_folder, batch_size=4, validation_split=0.2, augment=Fals
 
 def load_sidd_data_gpu(root_folder, batch_size=4, validation_split=0.2, augment=False, dataset_percentage=1.0,
                        only_validation=False, use_rgb=False, patch_size=256, seed=0, device="cuda", pool=None):
-    """``SIDD_dataset.load_data`` (SIDD_dataset.py:99-168) with device-side batches."""
+    """``SIDD_dataset.load_data`` (SIDD_dataset.py:99-168) with device-side batches.
+    ``patch_size=(128, 256)``: config 5's mixed patch stream (MixedPatchLoader)."""
+    if pool is None and not isinstance(patch_size, (int, np.integer)):
+        pairs = sidd_pairs(root_folder)
+        gts = [_read_image(g, use_rgb) for _, g in pairs]
+        noisy = [_read_image(n, use_rgb) for n, _ in pairs]
+        return _mixed(lambda ps: load_sidd_data_gpu(root_folder, batch_size, validation_split, augment,
+                                                    dataset_percentage, only_validation, use_rgb, ps, seed, device,
+                                                    pool=PatchPool(gts, ps, device, noisy_images=noisy)),
+                      patch_size)
     pool = pool or PatchPool.from_sidd(root_folder, use_rgb, patch_size, device)
     if only_validation:
         return None, GpuLoader(pool, range(len(pool)), batch_size, None, False, augment, seed)

@@ -140,3 +140,27 @@ class TrainStepGraph:
         self.graph.replay()
         self.opt._replayed()
         return self.loss
+
+
+class TrainStepGraphs:
+    """One captured train step per input shape (config 5's mixed 128/256 patch
+    stream, synth.MixedPatchLoader): a batch of a new shape captures its own
+    TrainStepGraph (its own engine, activations and graph); the graphs share the
+    model's flat parameters, gradient buffer and the optimizer's state (Adam moments
+    and the device step counter), and replays run one after another on the stream,
+    so the alternation is the same sequence of steps as eager training."""
+
+    def __init__(self, model, optimizer, distribution_choice='uniform', clip_value=1.0, t_input=False, warmup=2):
+        self.model, self.opt = model, optimizer
+        self.kw = dict(distribution_choice=distribution_choice, clip_value=clip_value, t_input=t_input,
+                       warmup=warmup)
+        self.graphs = {}
+        self.captures = 0
+
+    def __call__(self, clean_images, noisy_images, t=None):
+        shape = tuple(clean_images.shape)
+        g = self.graphs.get(shape)
+        if g is None:
+            g = self.graphs[shape] = TrainStepGraph(self.model, self.opt, shape, **self.kw)
+            self.captures += 1
+        return g(clean_images, noisy_images, t)
