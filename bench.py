@@ -136,10 +136,28 @@ def cpu_baseline(seconds=12.0, batch=16, size=256, steps=3):
         R.train_step(params, clean, noisy, t, 20)
         ts.append(time.perf_counter() - t0)
     med = sorted(ts)[len(ts) // 2]
+    # BASELINE.md "What is timed" legs 2-3: the reference's own batch-2 step (SURVEY §6's
+    # 2.02 img/s on 8 vCPU) and its published inference timing, improved_sampling
+    # (T = 20: 40 UNet forwards) on one 256x256 image (evaluate_model.py:126-133)
+    t2 = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        R.train_step(params, clean[:2], noisy[:2], t[:2], 20)
+        t2.append(time.perf_counter() - t0)
+    med2 = sorted(t2)[1]
+    x1 = noisy[:1]
+    with torch.no_grad():
+        t0 = time.perf_counter()
+        R.improved_sampling(lambda xx, tt: R.rdunet_t_forward(params, xx, tt), x1, 20)
+        t_samp = time.perf_counter() - t0
     return {"value": round(batch / med, 4), "unit": "images/s", "cores": torch.get_num_threads(),
             "kind": "port", "step_s_median": round(med, 3), "step_s_all": [round(x, 3) for x in ts],
+            "train_step_b2": {"images_per_s": round(2 / med2, 4), "step_s_median": round(med2, 3),
+                              "step_s_all": [round(x, 3) for x in t2]},
+            "improved_sampling_256_b1_s": round(t_samp, 3),
             "sample": f"median of {len(ts)} oracle train steps (fwd+Charbonnier+bwd+clip) of RDUNet_T(32) fp32 at "
-                      f"batch {batch} x 3x{size}x{size} on the host CPU ({sum(ts):.1f}s timed)"}
+                      f"batch {batch} x 3x{size}x{size} on the host CPU ({sum(ts):.1f}s timed); also the batch-2 "
+                      f"step (median of 3) and one improved_sampling call (T=20) on 1x3x{size}x{size}"}
 
 
 def config1_forward(dev, reps=5):
