@@ -161,10 +161,17 @@ int64_t rdn_wgrad_workspace_size(const rdn_wgrad_desc* d);
 int rdn_wgrad_reduce(const float* ws, int32_t splits, int32_t mdim, int32_t ndim, int32_t ndim_real,
                      int32_t taps, float* grad, int32_t accumulate,
                      const float* part, int32_t part_splits, float* dalpha, float* dbias, void* stream);
+/* the same for slabs that hold a slice of the input channels: grad[(m*grad_ci_total +
+   grad_ci0 + nd)*taps + tap] (+)= sum_s ws[s][m][tap*ndim + nd] for nd < ndim (the column
+   halves of rdn_conv_dgrad_wgrad, rdn_conv_dgrad_wgrad_cols) */
+int rdn_wgrad_reduce_cols(const float* ws, int32_t splits, int32_t mdim, int32_t ndim, int32_t taps, float* grad,
+                          int32_t grad_ci_total, int32_t grad_ci0, int32_t accumulate, const float* part,
+                          int32_t part_splits, float* dalpha, float* dbias, void* stream);
 
 /* Fused input gradient + weight gradient of one gated 3x3 conv (the narrow level-0
    layers: dgrad->cin = 16|32 dY channels, dgrad->ncols = wgrad->ndim = 32..80 input
-   channels, full 8x16 tiles, bf16): ONE pass over the gated dY (dgrad->gate must be
+   channels; and, in two column halves, the level-1 conv_1 / conv_2 with 32 dY and 96 /
+   128 input channels; full 8x16 tiles, bf16): ONE pass over the gated dY (dgrad->gate must be
    set and equal wgrad->a_gate; wgrad->a must be dgrad->x) computes
    rdn_conv_fwd(dgrad) and rdn_conv_wgrad(wgrad) together, i.e. aten
    convolution_backward's grad_input and grad_weight of Unet_model.py:72-89 with
@@ -174,6 +181,11 @@ int rdn_wgrad_reduce(const float* ws, int32_t splits, int32_t mdim, int32_t ndim
 int rdn_conv_dgrad_wgrad(const rdn_conv_desc* dgrad, const rdn_wgrad_desc* wgrad, void* stream);
 /* split count (weight-gradient slabs) the fused kernel writes for the pair; 0 = not served */
 int rdn_conv_dgrad_wgrad_splits(const rdn_conv_desc* dgrad, const rdn_wgrad_desc* wgrad);
+/* input channels per weight-gradient slab: wgrad->ndim, or ndim/2 for the column-half
+   launches, whose slabs [h*splits/2, (h+1)*splits/2) hold channels [h*ndim/2, ...) (sum
+   each half with rdn_wgrad_reduce_cols; the dalpha/dbias partials are in half 0's rows,
+   half 1's are zero); 0 = not served */
+int rdn_conv_dgrad_wgrad_cols(const rdn_conv_desc* dgrad, const rdn_wgrad_desc* wgrad);
 /* name of the fused kernel instantiation (1 = not served) */
 int rdn_conv_dgrad_wgrad_kernel_name(const rdn_conv_desc* dgrad, const rdn_wgrad_desc* wgrad, char* buf, int32_t len);
 

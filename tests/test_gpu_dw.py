@@ -9,7 +9,9 @@ into fp32 split-K partials (one slab per persistent block instead of the rows
 kernel's ranges), i.e. by fp32 summation order: rel-L2 <= 1e-5 per tensor (measured
 on MI355X below 1e-6).  Network: RDUNet_T (Unet_model.py:133-166) in bf16 at a
 full 256-wide level 0 and at small sizes, where the ragged XCD tile ranges leave
-some blocks without tiles (zero slabs)."""
+some blocks without tiles (zero slabs).  The level-1 conv_1 / conv_2 run as column
+halves (two blocks per tile, 48 / 64 of their 96 / 128 input channels each) against
+the gated-free separate path (PReLU-backward pass, conv3_big dgrad, wgrad3_glds)."""
 import pytest
 import torch
 
@@ -54,6 +56,8 @@ def test_fused_dgrad_wgrad_matches_separate(B, S):
     y1, g1, n1 = _grads(True, B, S)
     assert not n0
     assert n1 and all(k.startswith("conv3_dw_kernel") for k in n1), n1
+    if S >= 64:   # level-1 conv_1 / conv_2 (96 / 128 input channels) in column halves
+        assert any(k.endswith(",h2>") for k in n1), n1
     assert torch.equal(y0, y1)
     worst = max(_rel(g1[k], g0[k]) for k in g0)
     assert worst <= 1e-5, sorted(((_rel(g1[k], g0[k]), k) for k in g0), reverse=True)[:5]

@@ -84,11 +84,13 @@ SIGNATURES = {
     "rdn_wgrad_splits": (_i32, [C.POINTER(WgradDesc)]),
     "rdn_conv_dgrad_wgrad": (_i32, [C.POINTER(ConvDesc), C.POINTER(WgradDesc), _vp]),
     "rdn_conv_dgrad_wgrad_splits": (_i32, [C.POINTER(ConvDesc), C.POINTER(WgradDesc)]),
+    "rdn_conv_dgrad_wgrad_cols": (_i32, [C.POINTER(ConvDesc), C.POINTER(WgradDesc)]),
     "rdn_conv_dgrad_wgrad_kernel_name": (_i32, [C.POINTER(ConvDesc), C.POINTER(WgradDesc), C.c_char_p, _i32]),
     "rdn_wgrad_chunks": (_i32, [C.POINTER(WgradDesc)]),
     "rdn_dense3_fwd": (_i32, [C.POINTER(Dense3Desc), _vp]),
     "rdn_wgrad_workspace_size": (_i64, [C.POINTER(WgradDesc)]),
     "rdn_wgrad_reduce": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _vp, _i32, _vp, _i32, _vp, _vp, _vp]),
+    "rdn_wgrad_reduce_cols": (_i32, [_vp, _i32, _i32, _i32, _i32, _vp, _i32, _i32, _i32, _vp, _i32, _vp, _vp, _vp]),
     "rdn_prelu_bwd_blocks": (_i32, [_i32, _i64, _i32]),
     "rdn_prelu_bwd": (_i32, [_i32, _i64, _i32, _i32, _i32, _i32, _i32, _vp, _i64, _i32, _i64, _vp, _vp, _i64, _vp,
                              _vp, _vp, _vp, _vp, _vp]),

@@ -40,6 +40,17 @@
 // Every global load in the tile loop is unconditional (out-of-image units read a
 // zero line), so the compiler's vmcnt waits count exactly and the wait for tile
 // t+1 does not drain tile t+2's loads.
+//
+// Column halves (NH = 2, round 4): the level-1 conv_1 / conv_2 (96 / 128 input
+// channels, 32 dY channels) in one pass as well.  A block serves one half of the
+// input channels, [col0, col0 + BN) with BN = ncols / 2, for every tile of its range:
+// its dX slice, the matching rows of the resident weight panel, its X channels and
+// its weight-gradient columns (tap, ci in the half: a slab of mdim x 9*BN, the
+// blocks of half h at slabs [h*G/2, (h+1)*G/2), summed by rdn_wgrad_reduce_cols).
+// Both halves gate the same dY tile; only half 0 counts the dalpha / dbias partials
+// (half 1 writes zero rows).  The whole 96 / 128-column tile would not fit: the
+// resident panel and the W waves' accumulators grow with the columns (<96,32>
+// spilled, r02).
 #include "conv3_tile.h"
 
 #include <stdlib.h>
@@ -94,7 +105,7 @@ struct DwCfg {
   static constexpr bool FITS = LDS <= LDS_MAX && D_BYTES + X_BYTES + CT_BYTES >= RED_BYTES;
 };
 
-template <int BN, int CK>
+template <int BN, int CK, int NH>
 __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wgrad_desc wg, int tiles_x, int tiles_y,
                                                          int ntiles) {
   using Cfg = DwCfg<BN, CK>;
@@ -131,12 +142,18 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
   const int H = d.h, W = d.w;
   const int flags = d.flags;
 
-  // this block's tiles: XCD share, strided by the XCD's block count (conv3_ws)
-  const int per = gridDim.x >> 3;
+  // this block's tiles: XCD share, strided by the XCD's block count (conv3_ws); with
+  // column halves the XCD's blocks alternate halves and each half strides its own
+  const int per = (gridDim.x >> 3) / NH;
   const int xcd = blockIdx.x & 7;
+  const int jb = blockIdx.x >> 3;
+  const int half = NH > 1 ? jb % NH : 0;
+  const int col0 = half * BN;                           // first input channel of this block's half
+  // weight-gradient slab / partial row of this block (halves: grouped by half)
+  const int slab = NH > 1 ? half * (gridDim.x / NH) + xcd * per + jb / NH : (int)blockIdx.x;
   const int t_lo = (int)((int64_t)ntiles * xcd / 8);
   const int t_hi = (int)((int64_t)ntiles * (xcd + 1) / 8);
-  int t = t_lo + (blockIdx.x >> 3);
+  int t = t_lo + jb / NH;
   const int t_last = t_hi - 1;                          // loads of a tile past the range re-read this one
 
   const bf16* __restrict__ DY = (const bf16*)d.x;
@@ -149,7 +166,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     constexpr int UPRW = KC / VEC;
     for (int u = tid; u < BN * UPRW; u += NT) {
       const int n = u / UPRW, k8 = u - n * UPRW;
-      *(u32x4*)(wl + n * WROW + k8 * 16) = *(const u32x4*)(WP + (int64_t)n * d.kp + k8 * VEC);
+      *(u32x4*)(wl + n * WROW + k8 * 16) = *(const u32x4*)(WP + (int64_t)(col0 + n) * d.kp + k8 * VEC);
     }
     for (int c = tid; c < CK; c += NT) alds[c] = d.gate_alpha[c];
   }
@@ -208,7 +225,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     bool eok[NTL];
 #pragma unroll
     for (int jn = 0; jn < NTL; ++jn) {
-      const int c = jn * 16 + 4 * g;
+      const int c = col0 + jn * 16 + 4 * g;
       eok[jn] = has_res ? c < d.res_climit : has_acc;
       coff_e[jn] = has_res ? rdn_coff32(d.res_c0 + c, (int)d.res_ps, (int)d.res_pl)
                            : rdn_coff32(d.out_c0 + c, (int)d.out_ps, (int)d.out_pl);
@@ -346,14 +363,14 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     if (t < t_hi) {
       load(t, lA, gA);
       load_epi(t, eC);
-      store(lA, gA, true, 0);
+      store(lA, gA, half == 0, 0);
       load(min(t + per, t_last), lA, gA);
     }
     __syncthreads();   // weights + first halos
     auto step = [&](u32x4 (&lc)[D_IT], u32x4 (&gc)[D_IT], const u32x2 (&ec)[MT][NTL], u32x2 (&en)[MT][NTL],
                     int cur) -> bool {
       const int t1 = t + per;
-      store(lc, gc, t1 < t_hi, (cur ^ 1) * Cfg::D_BYTES);   // (past the range: a re-read of the last tile)
+      store(lc, gc, half == 0 && t1 < t_hi, (cur ^ 1) * Cfg::D_BYTES);   // (past the range: a re-read of the last tile)
       load(min(t + 2 * per, t_last), lc, gc);
       load_epi(min(t1, t_last), en);
       dgrad_tile(t, ec, cur * Cfg::D_BYTES);   // MFMAs + dX stores
@@ -367,7 +384,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     if (t < t_hi) {
       load(t, lA, gA);
       load_epi(t, eC);
-      store(lA, gA, true, 0);
+      store(lA, gA, half == 0, 0);
       load(min(t + per, t_last), lA, gA);
     }
     __syncthreads();   // weights + first halos
@@ -378,7 +395,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       load_epi(min(t1, t_last), en);
       dgrad_tile(t, ec, 0);   // MFMAs + dX stores
       __syncthreads();   // halos of t consumed
-      store(lc, gc, t1 < t_hi, 0);   // unconditional (past the range: a re-read of the last tile)
+      store(lc, gc, half == 0 && t1 < t_hi, 0);   // unconditional (past the range: a re-read of the last tile)
       __syncthreads();   // halos of t1 visible
       t = t1;
       return t < t_hi;
@@ -398,7 +415,8 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     }
   } else {
     // ================= W waves: X halo, wgrad
-    const int xupp = (wg.b_pl && wg.b_c0 % wg.b_ps == 0 && XU % (wg.b_ps / VEC) == 0) ? (int)(wg.b_ps / VEC) : XU;
+    const int xc0 = wg.b_c0 + col0;
+    const int xupp = (wg.b_pl && xc0 % wg.b_ps == 0 && XU % (wg.b_ps / VEC) == 0) ? (int)(wg.b_ps / VEC) : XU;
     // per unit: global offset and LDS offset (-1: padding unit; its halo pixel is
     // llds / XROW, so no third array)
     int lrel[X_IT], llds[X_IT];
@@ -409,7 +427,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       const bool ok = u < X_UNITS;
       const int hq = ok ? rem / xupp : 0, cu = ok ? pln * xupp + rem % xupp : 0;
       const int hy = hq / RS, hx = hq - hy * RS;
-      lrel[it] = (hy * W + hx) * (int)wg.b_ps + rdn_coff32(wg.b_c0 + cu * VEC, (int)wg.b_ps, (int)wg.b_pl);
+      lrel[it] = (hy * W + hx) * (int)wg.b_ps + rdn_coff32(xc0 + cu * VEC, (int)wg.b_ps, (int)wg.b_pl);
       llds[it] = ok ? hq * XROW + cu * 16 : -1;
     }
     auto load = [&](int tt, u32x4 (&lr)[X_IT]) {
@@ -606,16 +624,18 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
 
     }
 
-    // this block's split of the weight gradient (zero slab for a block without tiles)
-    const int ncol_all = 9 * wg.ndim;
-    float* __restrict__ ws = wg.ws + (int64_t)blockIdx.x * wg.mdim * ncol_all;
+    // this block's split of the weight gradient (zero slab for a block without tiles);
+    // halves: the slab holds this half's 9 x BN columns only
+    const int ncolw = NH > 1 ? BN : wg.ndim;
+    const int ncol_all = 9 * ncolw;
+    float* __restrict__ ws = wg.ws + (int64_t)slab * wg.mdim * ncol_all;
 #pragma unroll
     for (int j = 0; j < NTW; ++j) {
       const int nt = rw + 4 * j;
       if (nt >= NT_ALL) continue;
       const int c = nt * 16 + r;
       const int tp = c / BN, ci = c - tp * BN;
-      const int col = tp * wg.ndim + ci;
+      const int col = tp * ncolw + ci;
 #pragma unroll
       for (int i = 0; i < MTW; ++i)
 #pragma unroll
@@ -640,8 +660,8 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
         b += red[NR * VEC + (rr * DUC + cg) * VEC + k];
       }
       if (rt < wg.mdim) {
-        wg.part[((int64_t)blockIdx.x * 2 + 0) * wg.mdim + rt] = a;
-        wg.part[((int64_t)blockIdx.x * 2 + 1) * wg.mdim + rt] = b;
+        wg.part[((int64_t)slab * 2 + 0) * wg.mdim + rt] = a;   // (zero rows in half 1)
+        wg.part[((int64_t)slab * 2 + 1) * wg.mdim + rt] = b;
       }
     }
   }
@@ -667,14 +687,19 @@ int device_cus() {
 }
 
 // blocks of the persistent grid = the weight-gradient split count: one per CU (a
-// multiple of 8: the XCD tile ranges), at most the tiles of an XCD's share
-int dw_grid(int ntiles) {
+// multiple of 8: the XCD tile ranges), at most the tiles of an XCD's share (per
+// column half: nh halves take nh blocks per XCD slot)
+int dw_grid(int ntiles, int nh = 1) {
   const int per_xcd = (ntiles + 7) / 8;
-  int slots = device_cus() / 8;
+  int slots = device_cus() / (8 * nh);
   if (slots > per_xcd) slots = per_xcd;
   if (slots < 1) slots = 1;
-  return 8 * slots;
+  return 8 * nh * slots;
 }
+
+// column halves for this pair: 2 for the 96 / 128-input-channel convs with 32 dY
+// channels (level-1 conv_1 / conv_2), else 1
+int dw_nh(const rdn_conv_desc* d) { return (d->cin == 32 && (d->ncols == 96 || d->ncols == 128)) ? 2 : 1; }
 
 // the pair this kernel serves (else 1 = run the separate dgrad / wgrad launches)
 bool dw_serves(const rdn_conv_desc* d, const rdn_wgrad_desc* wg) {
@@ -685,7 +710,8 @@ bool dw_serves(const rdn_conv_desc* d, const rdn_wgrad_desc* wg) {
   if ((d->flags & RDN_EPI_RESID) && (d->flags & RDN_EPI_ACCUM)) return false;
   if (d->h % TH || d->w % TW || d->n != wg->n || d->h != wg->h || d->w != wg->w) return false;
   if (d->cin != 16 && d->cin != 32) return false;
-  if (d->ncols != d->cout || d->ncols % 16 || d->ncols < 32 || d->ncols > 80 || wg->ndim != d->ncols) return false;
+  const int nh = dw_nh(d);
+  if (d->ncols != d->cout || d->ncols % 16 || d->ncols < 32 || d->ncols / nh > 80 || wg->ndim != d->ncols) return false;
   if (wg->mdim > d->cin || wg->mdim <= 0 || wg->b_c0 % 8 || wg->b_ps % 8 || ((uintptr_t)wg->b & 15)) return false;
   // the same gated operand on both sides
   if (wg->a != d->x || wg->a_ps != d->x_ps || wg->a_c0 != d->x_c0 || wg->a_pl != d->x_pl || wg->a_gate != d->gate ||
@@ -711,21 +737,22 @@ bool dw_serves(const rdn_conv_desc* d, const rdn_wgrad_desc* wg) {
   return nt < (1ll << 31);
 }
 
-template <int BN, int CK>
+template <int BN, int CK, int NH = 1>
 int launch_dw(const rdn_conv_desc* d, const rdn_wgrad_desc* wg, hipStream_t st) {
   if constexpr (!DwCfg<BN, CK>::FITS) {
     return 1;
   } else {
     const int tiles_x = d->w / TW, tiles_y = d->h / TH;
     const int ntiles = d->n * tiles_x * tiles_y;
-    const int grid = dw_grid(ntiles);
+    const int grid = dw_grid(ntiles, NH);
+    if (NH > 1) RDN_PROBE("conv3_dw_kernel<bf16,%d,%d,h%d>", BN, CK, NH);
     RDN_PROBE("conv3_dw_kernel<bf16,%d,%d>", BN, CK);
     if (wg->splits != grid) {
       rdn_set_error("rdn_conv_dgrad_wgrad: wgrad splits %d != %d (rdn_conv_dgrad_wgrad_splits)", wg->splits, grid);
       return RDN_E_ARG;
     }
     if (!wg->ws) { rdn_set_error("rdn_conv_dgrad_wgrad: null workspace"); return RDN_E_ARG; }
-    hipLaunchKernelGGL((conv3_dw_kernel<BN, CK>), dim3((unsigned)grid), dim3(NT), 0, st, *d, *wg, tiles_x, tiles_y,
+    hipLaunchKernelGGL((conv3_dw_kernel<BN, CK, NH>), dim3((unsigned)grid), dim3(NT), 0, st, *d, *wg, tiles_x, tiles_y,
                        ntiles);
     return rdn_check_launch("rdn_conv_dgrad_wgrad");
   }
@@ -733,6 +760,15 @@ int launch_dw(const rdn_conv_desc* d, const rdn_wgrad_desc* wg, hipStream_t st) 
 
 template <int CK>
 int dw_bn(const rdn_conv_desc* d, const rdn_wgrad_desc* wg, hipStream_t st) {
+  if constexpr (CK == 32) {
+    if (dw_nh(d) == 2) {
+      switch (d->ncols) {
+        case 96: return launch_dw<48, 32, 2>(d, wg, st);
+        case 128: return launch_dw<64, 32, 2>(d, wg, st);
+      }
+      return 1;
+    }
+  }
   switch (d->ncols) {
     case 32: return launch_dw<32, CK>(d, wg, st);
     case 48: return launch_dw<48, CK>(d, wg, st);
@@ -766,7 +802,14 @@ extern "C" int rdn_conv_dgrad_wgrad_splits(const rdn_conv_desc* dgrad, const rdn
   const int rc = dw_dispatch(dgrad, wgrad, nullptr);   // instantiation exists for this shape?
   rdn_probe_buf = nullptr;
   if (rc != 0) return 0;
-  return dw_grid(dgrad->n * (dgrad->h / TH) * (dgrad->w / TW));
+  return dw_grid(dgrad->n * (dgrad->h / TH) * (dgrad->w / TW), dw_nh(dgrad));
+}
+
+// input channels per weight-gradient slab (= wgrad->ndim, or ndim / 2 with column
+// halves: the slabs of half h are [h*splits/2, (h+1)*splits/2)), 0 if not served
+extern "C" int rdn_conv_dgrad_wgrad_cols(const rdn_conv_desc* dgrad, const rdn_wgrad_desc* wgrad) {
+  if (!rdn_conv_dgrad_wgrad_splits(dgrad, wgrad)) return 0;
+  return dgrad->ncols / dw_nh(dgrad);
 }
 
 extern "C" int rdn_conv_dgrad_wgrad_kernel_name(const rdn_conv_desc* dgrad, const rdn_wgrad_desc* wgrad, char* buf,

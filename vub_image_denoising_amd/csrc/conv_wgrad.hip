@@ -193,7 +193,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
                                                            int ndim_real, int taps, float* __restrict__ grad,
                                                            int accumulate, int sl_count, const float* __restrict__ part,
                                                            int part_splits, float* __restrict__ dalpha,
-                                                           float* __restrict__ dbias) {
+                                                           float* __restrict__ dbias, int gstride, int gci0) {
   if (blockIdx.y == 1) {  // fused-PReLU partials: one block per (channel, dalpha|dbias), fixed order
     if (blockIdx.x >= 2 * mdim) return;
     const int which = blockIdx.x / mdim, m = blockIdx.x - which * mdim;
@@ -244,7 +244,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
       const int col = col0 + e;
       const int tap = col / ndim, nd = col - tap * ndim;
       if (nd < ndim_real) {
-        const int64_t dst = ((int64_t)m * ndim_real + nd) * taps + tap;
+        const int64_t dst = ((int64_t)m * gstride + gci0 + nd) * taps + tap;
         grad[dst] = accumulate ? grad[dst] + s[e] : s[e];
       }
     }
@@ -342,10 +342,11 @@ extern "C" int rdn_conv_wgrad(const rdn_wgrad_desc* d, void* stream) {
   return d->dtype == RDN_BF16 ? launch_t<bf16>(d, st) : launch_t<float>(d, st);
 }
 
-extern "C" int rdn_wgrad_reduce(const float* ws, int32_t splits, int32_t mdim, int32_t ndim, int32_t ndim_real,
-                                int32_t taps, float* grad, int32_t accumulate, const float* part, int32_t part_splits,
-                                float* dalpha, float* dbias, void* stream) {
-  if (!ws || !grad || splits <= 0 || mdim <= 0 || ndim <= 0 || ndim_real <= 0 || ndim_real > ndim || taps <= 0) {
+static int wgrad_reduce_impl(const float* ws, int32_t splits, int32_t mdim, int32_t ndim, int32_t ndim_real,
+                             int32_t taps, float* grad, int32_t gstride, int32_t gci0, int32_t accumulate,
+                             const float* part, int32_t part_splits, float* dalpha, float* dbias, void* stream) {
+  if (!ws || !grad || splits <= 0 || mdim <= 0 || ndim <= 0 || ndim_real <= 0 || ndim_real > ndim || taps <= 0 ||
+      gci0 < 0 || gci0 + ndim_real > gstride) {
     rdn_set_error("rdn_wgrad_reduce: bad arguments"); return RDN_E_ARG;
   }
   const int64_t total = (int64_t)mdim * ndim * taps;
@@ -364,6 +365,21 @@ extern "C" int rdn_wgrad_reduce(const float* ws, int32_t splits, int32_t mdim, i
   dim3 grid((unsigned)blocks, part ? 2 : 1);
   wgrad_reduce_kernel<<<grid, 256, 0, (hipStream_t)stream>>>(ws, splits, mdim, ndim, ndim_real, taps, grad, accumulate,
                                                             sl, part, part_splits > 0 ? part_splits : splits, dalpha,
-                                                            dbias);
+                                                            dbias, gstride, gci0);
   return rdn_check_launch("rdn_wgrad_reduce");
+}
+
+extern "C" int rdn_wgrad_reduce(const float* ws, int32_t splits, int32_t mdim, int32_t ndim, int32_t ndim_real,
+                                int32_t taps, float* grad, int32_t accumulate, const float* part, int32_t part_splits,
+                                float* dalpha, float* dbias, void* stream) {
+  return wgrad_reduce_impl(ws, splits, mdim, ndim, ndim_real, taps, grad, ndim_real, 0, accumulate, part, part_splits,
+                           dalpha, dbias, stream);
+}
+
+extern "C" int rdn_wgrad_reduce_cols(const float* ws, int32_t splits, int32_t mdim, int32_t ndim, int32_t taps,
+                                     float* grad, int32_t grad_ci_total, int32_t grad_ci0, int32_t accumulate,
+                                     const float* part, int32_t part_splits, float* dalpha, float* dbias,
+                                     void* stream) {
+  return wgrad_reduce_impl(ws, splits, mdim, ndim, ndim, taps, grad, grad_ci_total, grad_ci0, accumulate, part,
+                           part_splits, dalpha, dbias, stream);
 }

@@ -756,78 +756,95 @@ class UNetEngine:
             # PReLU backward inside their dgrad / wgrad loaders (gate = saved
             # PReLU input); the output conv (NCHW dy) and the 2x2 convs keep
             # the separate rdn_prelu_bwd pass producing dYpre.
-            fused = (L.kind == "c3" and L.ddst is not None) and FUSE_PRELU
+            gate_ok = (L.kind == "c3" and L.ddst is not None) and FUSE_PRELU
+            fused = gate_ok
             if fused:  # only when the wgrad reads operand A (with the gate) in one chunk
                 n_, h_, w_ = self.grid[L.level]
                 probe = H.WgradDesc(dtype=self.code, gather=H.RDN_G_CONV3, n=n_, h=h_, w=w_, hin=h_, win=w_,
                                     mdim=L.cout, ndim=L.cin_pad)
                 fused = lib.rdn_wgrad_chunks(C.byref(probe)) == 1
-            L.extra["fused"] = fused
             pre = self.bufs[L.pre]
             alpha = self.named[L.act + ".weight"]
-            # --- input gradient (dgrad) as a forward-shaped conv over dYpre
-            d = H.ConvDesc()
-            d.dtype = self.code
-            packed = L.pack_dgrad[8]
-            d.wp, d.kp = packed.data_ptr(), packed.shape[1]
-            d.x, d.x_c0 = dyp, 0
-            flags = 0
-            if L.kind == "c3":
-                n, h, w = self.grid[L.level]
-                d.gather, d.hin, d.win = H.RDN_G_CONV3, h, w
-                d.x_ps, d.cin = L.cout_pad, L.cout_pad
-                d.ncols = d.cout = L.cin
-                if fused:
-                    d.x, d.x_ps, d.x_c0, d.x_pl = self._slice(L.ddst)
-                    d.gate, d.gate_ps, d.gate_alpha = pre.data_ptr(), pre.shape[1], alpha.data_ptr()
-            elif L.kind == "down":       # per-pixel GEMM on the low-res grid, scattered to 2x2
-                n, h, w = self.grid[L.level]
-                d.gather, d.hin, d.win = H.RDN_G_PIX, h, w
-                d.x_ps, d.cin = L.cout, L.cout
-                d.ncols, d.cout = 4 * L.cin, L.cin
-                flags |= H.EPI_SCATTER2
-            else:                        # conv-s2 gather of the hi-res dYpre
-                n, h, w = self.grid[L.level]
-                d.gather, d.hin, d.win = H.RDN_G_S2, 2 * h, 2 * w
-                d.x_ps, d.cin = L.cout, L.cout
-                d.ncols = d.cout = L.cin
-            d.n, d.h, d.w = n, h, w
-            d.out, d.out_ps, d.out_c0, d.out_pl = self._slice(L.dsrc)
-            if L.accum:
-                flags |= H.EPI_ACCUM
-            if L.resid is not None:      # d(x) += dOut through "out_3 + x" (Unet_model.py:89)
-                flags |= H.EPI_RESID
-                d.res, d.res_ps, d.res_c0, d.res_pl = self._slice(L.ddst)
-                d.res_climit = L.resid_c
-            d.flags = flags
+            pure = L.src.buf in self.pure_inputs
+
+            def build(fused):
+                # --- input gradient (dgrad) as a forward-shaped conv over dYpre
+                d = H.ConvDesc()
+                d.dtype = self.code
+                packed = L.pack_dgrad[8]
+                d.wp, d.kp = packed.data_ptr(), packed.shape[1]
+                d.x, d.x_c0 = dyp, 0
+                flags = 0
+                if L.kind == "c3":
+                    n, h, w = self.grid[L.level]
+                    d.gather, d.hin, d.win = H.RDN_G_CONV3, h, w
+                    d.x_ps, d.cin = L.cout_pad, L.cout_pad
+                    d.ncols = d.cout = L.cin
+                    if fused:
+                        d.x, d.x_ps, d.x_c0, d.x_pl = self._slice(L.ddst)
+                        d.gate, d.gate_ps, d.gate_alpha = pre.data_ptr(), pre.shape[1], alpha.data_ptr()
+                elif L.kind == "down":       # per-pixel GEMM on the low-res grid, scattered to 2x2
+                    n, h, w = self.grid[L.level]
+                    d.gather, d.hin, d.win = H.RDN_G_PIX, h, w
+                    d.x_ps, d.cin = L.cout, L.cout
+                    d.ncols, d.cout = 4 * L.cin, L.cin
+                    flags |= H.EPI_SCATTER2
+                else:                        # conv-s2 gather of the hi-res dYpre
+                    n, h, w = self.grid[L.level]
+                    d.gather, d.hin, d.win = H.RDN_G_S2, 2 * h, 2 * w
+                    d.x_ps, d.cin = L.cout, L.cout
+                    d.ncols = d.cout = L.cin
+                d.n, d.h, d.w = n, h, w
+                d.out, d.out_ps, d.out_c0, d.out_pl = self._slice(L.dsrc)
+                if L.accum:
+                    flags |= H.EPI_ACCUM
+                if L.resid is not None:      # d(x) += dOut through "out_3 + x" (Unet_model.py:89)
+                    flags |= H.EPI_RESID
+                    d.res, d.res_ps, d.res_c0, d.res_pl = self._slice(L.ddst)
+                    d.res_climit = L.resid_c
+                d.flags = flags
+                # --- weight gradient
+                wg = H.WgradDesc()
+                wg.dtype = self.code
+                if L.kind == "c3":
+                    n, h, w = self.grid[L.level]
+                    wg.gather, wg.n, wg.h, wg.w, wg.hin, wg.win = H.RDN_G_CONV3, n, h, w, h, w
+                    wg.a, wg.a_ps, wg.a_c0, wg.mdim = dyp, L.cout_pad, 0, L.cout
+                    wg.b, wg.b_ps, wg.b_c0, wg.b_pl = self._slice(L.src)
+                    wg.ndim = L.cin_pad
+                    taps, ndim_real = 9, L.cin
+                    if fused:
+                        wg.a, wg.a_ps, wg.a_c0, wg.a_pl = self._slice(L.ddst)
+                        wg.a_gate, wg.a_gate_ps, wg.a_gate_alpha = pre.data_ptr(), pre.shape[1], alpha.data_ptr()
+                elif L.kind == "down":
+                    n, h, w = self.grid[L.level]
+                    wg.gather, wg.n, wg.h, wg.w, wg.hin, wg.win = H.RDN_G_S2, n, h, w, 2 * h, 2 * w
+                    wg.a, wg.a_ps, wg.a_c0, wg.mdim = dyp, L.cout, 0, L.cout
+                    wg.b, wg.b_ps, wg.b_c0, wg.b_pl = self._slice(L.src)
+                    wg.ndim = L.cin
+                    taps, ndim_real = 4, L.cin
+                else:
+                    n, h, w = self.grid[L.level]
+                    wg.gather, wg.n, wg.h, wg.w, wg.hin, wg.win = H.RDN_G_S2, n, h, w, 2 * h, 2 * w
+                    wg.a, wg.a_ps, wg.a_c0, wg.a_pl = self._slice(L.src)
+                    wg.mdim = L.cin
+                    wg.b, wg.b_ps, wg.b_c0, wg.ndim = dyp, L.cout, 0, L.cout
+                    taps, ndim_real = 4, L.cout
+                return d, wg, taps, ndim_real
+
+            d, wg, taps, ndim_real = build(fused)
+            dw = 0
+            if gate_ok and FUSE_DW and not pure:
+                # the fused dgrad + wgrad kernel gates in its own loader, also for the
+                # multi-chunk level-1 convs (column halves, rdn_conv_dgrad_wgrad_cols)
+                dg, wgg, _, _ = (d, wg, taps, ndim_real) if fused else build(True)
+                wgg.splits = 0
+                wgg.splits = lib.rdn_wgrad_splits(C.byref(wgg))
+                dw = lib.rdn_conv_dgrad_wgrad_splits(C.byref(dg), C.byref(wgg))
+                if dw > 0 and not fused:
+                    fused, d, wg = True, dg, wgg
+            L.extra["fused"] = fused
             L.dgrad_desc = d
-            # --- weight gradient
-            wg = H.WgradDesc()
-            wg.dtype = self.code
-            if L.kind == "c3":
-                n, h, w = self.grid[L.level]
-                wg.gather, wg.n, wg.h, wg.w, wg.hin, wg.win = H.RDN_G_CONV3, n, h, w, h, w
-                wg.a, wg.a_ps, wg.a_c0, wg.mdim = dyp, L.cout_pad, 0, L.cout
-                wg.b, wg.b_ps, wg.b_c0, wg.b_pl = self._slice(L.src)
-                wg.ndim = L.cin_pad
-                taps, ndim_real = 9, L.cin
-                if fused:
-                    wg.a, wg.a_ps, wg.a_c0, wg.a_pl = self._slice(L.ddst)
-                    wg.a_gate, wg.a_gate_ps, wg.a_gate_alpha = pre.data_ptr(), pre.shape[1], alpha.data_ptr()
-            elif L.kind == "down":
-                n, h, w = self.grid[L.level]
-                wg.gather, wg.n, wg.h, wg.w, wg.hin, wg.win = H.RDN_G_S2, n, h, w, 2 * h, 2 * w
-                wg.a, wg.a_ps, wg.a_c0, wg.mdim = dyp, L.cout, 0, L.cout
-                wg.b, wg.b_ps, wg.b_c0, wg.b_pl = self._slice(L.src)
-                wg.ndim = L.cin
-                taps, ndim_real = 4, L.cin
-            else:
-                n, h, w = self.grid[L.level]
-                wg.gather, wg.n, wg.h, wg.w, wg.hin, wg.win = H.RDN_G_S2, n, h, w, 2 * h, 2 * w
-                wg.a, wg.a_ps, wg.a_c0, wg.a_pl = self._slice(L.src)
-                wg.mdim = L.cin
-                wg.b, wg.b_ps, wg.b_c0, wg.ndim = dyp, L.cout, 0, L.cout
-                taps, ndim_real = 4, L.cout
             wg.splits = 0
             splits = lib.rdn_wgrad_splits(C.byref(wg))
             wg.splits = splits
@@ -836,9 +853,11 @@ class UNetEngine:
                 dw = lib.rdn_conv_dgrad_wgrad_splits(C.byref(d), C.byref(wg))
             L.extra["dw"] = dw > 0
             L.extra["dw_bytes"] = 0
+            L.extra["dw_cols"] = wg.ndim
             if dw > 0:   # the fused kernel's slabs: one per block of its persistent grid
                 splits = wg.splits = dw
                 L.extra["dw_bytes"] = dw * wg.mdim * 9 * wg.ndim * 4
+                L.extra["dw_cols"] = lib.rdn_conv_dgrad_wgrad_cols(C.byref(d), C.byref(wg))
             else:
                 ws_need = max(ws_need, lib.rdn_wgrad_workspace_size(C.byref(wg)))
             # dalpha / dbias partials: the fused loaders' per-split rows, else the
@@ -1165,8 +1184,20 @@ class UNetEngine:
             part_splits = (0 if fused else L.extra["part_rows"] if "gated_by" in L.extra
                            else lib.rdn_prelu_bwd_blocks(self.code, P, L.cout_pad))
             ow, ob, oa = L.extra["goff"]
-            rc = lib.rdn_wgrad_reduce(L.wgrad_desc.ws, splits, mdim, ndim, ndim_real, taps, gbase + ow, 1, pws,
-                                      part_splits, gbase + oa, gbase + ob, rst)
+            cols = L.extra["dw_cols"]
+            if cols < ndim:
+                # column halves of the fused kernel: each half's slabs hold its input
+                # channels; the dalpha/dbias partials are half 0's rows
+                nh, sh = ndim // cols, splits // (ndim // cols)
+                for hh in range(nh):
+                    rc = lib.rdn_wgrad_reduce_cols(L.wgrad_desc.ws + hh * sh * mdim * taps * cols * 4, sh, mdim, cols,
+                                                   taps, gbase + ow, ndim_real, hh * cols, 1,
+                                                   pws if hh == 0 else None, sh, gbase + oa, gbase + ob, rst)
+                    if rc:
+                        break
+            else:
+                rc = lib.rdn_wgrad_reduce(L.wgrad_desc.ws, splits, mdim, ndim, ndim_real, taps, gbase + ow, 1, pws,
+                                          part_splits, gbase + oa, gbase + ob, rst)
             if rc:
                 H.check(rc, f"wgrad_reduce[{L.name}]")
             if side is not None:
