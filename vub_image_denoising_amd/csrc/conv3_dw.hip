@@ -699,7 +699,17 @@ int dw_grid(int ntiles, int nh = 1) {
 
 // column halves for this pair: 2 for the 96 / 128-input-channel convs with 32 dY
 // channels (level-1 conv_1 / conv_2), else 1
-int dw_nh(const rdn_conv_desc* d) { return (d->cin == 32 && (d->ncols == 96 || d->ncols == 128)) ? 2 : 1; }
+// (RDN_DW_HALVES=0: only the single-tile shapes, for A/B)
+bool dw_halves_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("RDN_DW_HALVES");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+int dw_nh(const rdn_conv_desc* d) {
+  return (dw_halves_enabled() && d->cin == 32 && (d->ncols == 96 || d->ncols == 128)) ? 2 : 1;
+}
 
 // the pair this kernel serves (else 1 = run the separate dgrad / wgrad launches)
 bool dw_serves(const rdn_conv_desc* d, const rdn_wgrad_desc* wg) {
