@@ -49,6 +49,7 @@ from oracle import rdunet_ref as R  # noqa: E402
 from oracle.weights import make_params  # noqa: E402
 
 FIXTURE = os.path.join(REPO, "tests", "golden", "psnr_sigma25_oracle.json")
+MIN_SEEDS = 130   # half-width <= 0.03 dB at sd ~0.17 dB
 
 
 def _stats(d):
@@ -101,32 +102,62 @@ def _psnr_leg(leg, params, data, n256, c256):
     return PP.psnr_per_image(den, data[3]), PP.psnr_per_image(den256, c256)
 
 
-@pytest.mark.timeout(1100)
+SHARDS = 4
+_STATE = {}
+
+
+def _prep(cfg, r):
+    """Host side of one seed (initial weights, data, the 256x256 held-out image)."""
+    a = argparse.Namespace(**dict(cfg, seed=r["seed"]))
+    params = make_params(R.param_shapes(cfg["base_filters"]), r["seed"])
+    data = PP.make_data(a)
+    n256, c256 = MK.eval_256(r["seed"], cfg["sigma"])
+    return params, data, n256, c256
+
+
+def _fixture():
+    if "fx" not in _STATE:
+        fx = json.load(open(FIXTURE))
+        assert len(fx["runs"]) >= MIN_SEEDS, "fixture incomplete"
+        _STATE["fx"] = fx
+        _STATE["legs"] = {dt: _Leg(dt, fx["config"]) for dt in ("fp32", "bf16")}
+        _STATE["d64"] = {dt: {} for dt in ("fp32", "bf16")}
+        _STATE["d256"] = {dt: {} for dt in ("fp32", "bf16")}
+    return _STATE["fx"]
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("shard", range(SHARDS))
+def test_psnr_sigma25_shard(shard):
+    """One quarter of the seeds (the legs train and denoise; host-side preparation of
+    the next seeds runs in a thread pool meanwhile)."""
+    import concurrent.futures as cf
+    fx = _fixture()
+    cfg, legs = fx["config"], _STATE["legs"]
+    runs = fx["runs"][shard::SHARDS]
+    with cf.ThreadPoolExecutor(3) as ex:
+        futs = [ex.submit(_prep, cfg, r) for r in runs]
+        for r, f in zip(runs, futs):
+            params, data, n256, c256 = f.result()
+            assert abs(PP.psnr_per_image(data[2], data[3]) - r["noisy"]) < 1e-9, "data differs from the fixture's"
+            for dt, leg in legs.items():
+                p64, p256 = _psnr_leg(leg, params, data, n256, c256)
+                _STATE["d64"][dt][r["seed"]] = p64 - r["oracle"]
+                _STATE["d256"][dt][r["seed"]] = p256 - r["oracle_256"]
+                if r is fx["runs"][0] and dt == "fp32":
+                    _STATE["state0"] = ({k: v.detach().cpu().clone() for k, v in leg.model.state_dict().items()}, data)
+
+
+@pytest.mark.timeout(300)
 def test_psnr_sigma25_paired_vs_oracle_fixture():
-    fx = json.load(open(FIXTURE))
-    cfg = fx["config"]
-    runs = fx["runs"]
-    assert len(runs) >= 130, "fixture incomplete"
-    legs = {dt: _Leg(dt, cfg) for dt in ("fp32", "bf16")}
-    out = {dt: [] for dt in legs}
-    out256 = {dt: [] for dt in legs}
-    state0 = None
-    for i, r in enumerate(runs):
-        a = argparse.Namespace(**cfg, seed=r["seed"])
-        params = make_params(R.param_shapes(cfg["base_filters"]), r["seed"])
-        data = PP.make_data(a)
-        n256, c256 = MK.eval_256(r["seed"], cfg["sigma"])
-        assert abs(PP.psnr_per_image(data[2], data[3]) - r["noisy"]) < 1e-9, "data differs from the fixture's"
-        for dt, leg in legs.items():
-            p64, p256 = _psnr_leg(leg, params, data, n256, c256)
-            out[dt].append(p64 - r["oracle"])
-            out256[dt].append(p256 - r["oracle_256"])
-            if i == 0 and dt == "fp32":
-                state0 = ({k: v.detach().cpu().clone() for k, v in leg.model.state_dict().items()}, data, p64)
+    fx = _fixture()
+    cfg, runs, legs = fx["config"], fx["runs"], _STATE["legs"]
+    for dt in legs:
+        assert len(_STATE["d64"][dt]) == len(runs), "a shard did not finish"
     # inference parity at identical weights: seed 0's GPU-trained fp32 weights denoised
     # (4 held-out images) by this build and by the oracle's own sampler on the host
-    sd, data, _ = state0
-    a4 = argparse.Namespace(**cfg, seed=runs[0]["seed"], eval_batch=4)
+    sd, data = _STATE["state0"]
+    a4 = argparse.Namespace(**dict(cfg, seed=runs[0]["seed"], eval_batch=4))
     data4 = tuple(x[:4] if j in (2, 3) else x for j, x in enumerate(data))
     m = legs["fp32"].model
     m.load_state_dict(sd)
@@ -134,8 +165,8 @@ def test_psnr_sigma25_paired_vs_oracle_fixture():
         gpu4 = PP.psnr_per_image(m.improved_sampling(data4[2].cuda()).cpu(), data4[3])
     torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count())
     ora4 = PP.oracle_eval_psnr(a4, sd, data4)
-    s = {dt: _stats(out[dt]) for dt in legs}
-    s256 = {dt: _stats(out256[dt]) for dt in legs}
+    s = {dt: _stats(list(_STATE["d64"][dt].values())) for dt in legs}
+    s256 = {dt: _stats(list(_STATE["d256"][dt].values())) for dt in legs}
     gain = float(np.mean([r["oracle"] - r["noisy"] for r in runs]))
     gain256 = float(np.mean([r["oracle_256"] - r["noisy_256"] for r in runs]))
     res = {"config": cfg, "seeds": len(runs), "oracle_gain_64_db": round(gain, 4), "oracle_gain_256_db": round(gain256, 4),
