@@ -69,6 +69,16 @@ def main():
                 r[lname] = min(r.get(lname, 1e9), round(us, 2))
         for lname, _ in libs:
             r[lname + "_tfs"] = round(flops / (r[lname] * 1e-6) / 1e12, 1)
+        # the reduced weight gradient of every build against the first one's
+        grads = []
+        for lname, lib in libs:
+            g = torch.zeros(m * nd * 9, device="cuda")
+            H.check(lib.rdn_conv_wgrad(C.byref(d), st), "wgrad")
+            H.check(lib.rdn_wgrad_reduce(d.ws, lib.rdn_wgrad_splits(C.byref(d)), m, nd, nd, 9, g.data_ptr(), 0, None, 0,
+                                         None, None, st), "reduce")
+            torch.cuda.synchronize()
+            grads.append(g)
+        r["bit_identical"] = all(torch.equal(grads[0], g) for g in grads[1:])
         rows.append(r)
         print(json.dumps(r), flush=True)
     if out:

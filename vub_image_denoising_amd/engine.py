@@ -1019,8 +1019,12 @@ class UNetEngine:
             if "dense3" in L.extra:
                 blk = L.name[:-len(".conv_0")]
                 parts = [by_name[f"{blk}.conv_{k}"].extra["info"]["fwd"] for k in range(3)]
+                # 6th entry: the fused launch's own minimal bytes (x read once, each
+                # conv's output and PReLU input written once: 32 + 3 x 32 channels)
+                Ls = [by_name[f"{blk}.conv_{k}"] for k in range(3)]
+                fused_min = es * self.P[0] * (Ls[0].cin + sum(2 * x.cout for x in Ls))
                 L.extra["info"]["dense3"] = ("fwd", f"{blk}.conv_0-2", "conv3_dense_kernel<bf16,32,16>",
-                                             sum(p[3] for p in parts), sum(p[4] for p in parts))
+                                             sum(p[3] for p in parts), sum(p[4] for p in parts), fused_min)
 
     # ------------------------------------------------------------------
     def forward(self, xs, t: torch.Tensor | None = None) -> torch.Tensor:
