@@ -41,6 +41,10 @@ namespace {
 
 __device__ __attribute__((aligned(64))) unsigned int g_big_zero[16];
 
+#ifndef BIG_PF
+#define BIG_PF 0   // 1: next k-step's fragments read before the current MFMAs (A/B)
+#endif
+
 template <int N>
 __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
@@ -219,6 +223,39 @@ __global__ __launch_bounds__(NTB, 2) void conv3_big_kernel(rdn_conv_desc d, int 
       for (int jn = 0; jn < NTL; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
   };
 
+#if BIG_PF
+  // LDS stage jj of a chunk (K stages 2jj, 2jj+1) from halo image ph, weights pbs, as a
+  // pipeline over its (up to) four 32-deep k-steps: the fragments of k-step q + 1 are
+  // read before the MFMAs of q (two fragment sets live; same MFMA order: bit-identical)
+  auto compute = [&](int jj, const unsigned char* ph, const unsigned char* pbs) {
+    auto valid = [&](int q) { return 2 * jj + (q >> 1) < SPC && (2 * jj + (q >> 1)) * 64 + (q & 1) * 32 < 9 * CK; };
+    u32x4 af[2][MT], bfr[2][NTL];
+    auto rd = [&](int q, int buf) {
+      const int k0 = (2 * jj + (q >> 1)) * 64 + (q & 1) * 32;
+      const int tap = k0 / CK, ksub = (k0 - tap * CK) / 32;
+      const int dy = tap / 3, dx = tap % 3;
+      const unsigned char* pa = ph + a_row0 + dy * RS * RB + a_off[ksub * 3 + dx];
+#pragma unroll
+      for (int i = 0; i < MT; ++i) af[buf][i] = *(const u32x4*)(pa + i * RS * RB);
+#pragma unroll
+      for (int jn = 0; jn < NTL; ++jn) bfr[buf][jn] = *(const u32x4*)(pbs + jn * 16 * RW + b_off[q]);
+    };
+    rd(0, 0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (!valid(q)) break;
+      if (q + 1 < 4 && valid(q + 1)) rd(q + 1, (q + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);   // next k-step's reads issued before these MFMAs
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int jn = 0; jn < NTL; ++jn)   // D[column][pixel]
+          acc[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bfr[q & 1][jn]),
+                                                               __builtin_bit_cast(bf16x8, af[q & 1][i]), acc[i][jn], 0,
+                                                               0, 0);
+    }
+  };
+#else
   // LDS stage jj of a chunk (K stages 2jj, 2jj+1) from halo image ph, weights pbs
   auto compute = [&](int jj, const unsigned char* ph, const unsigned char* pbs) {
 #pragma unroll
@@ -248,6 +285,7 @@ __global__ __launch_bounds__(NTB, 2) void conv3_big_kernel(rdn_conv_desc d, int 
       }
     }
   };
+#endif
 
   // ---- epilogue: straight from the accumulators, through buffer descriptors on the
   // item's first pixel (32-bit offsets: few registers; pixels past the image edge get
