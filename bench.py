@@ -743,6 +743,7 @@ def main():
             "fp32_images_per_s": extra["fp32"]["images_per_s"] if extra else None,
             "extra_configs": extra,
             "roofline": roof,
+            "peak_hbm_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 2),
             "cpu_baseline": cpu,
             "inference": infer,
         }

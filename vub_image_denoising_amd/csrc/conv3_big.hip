@@ -108,6 +108,10 @@ __device__ __forceinline__ void wait_split(int wave) {   // vmcnt(wave < SPLIT ?
   else wait_vm<NLO>();
 }
 
+// launch bounds: 512 threads = 8 waves = two per SIMD, i.e. one block per CU (the LDS
+// budget allows no more); the second argument is waves per SIMD (EU), so the register
+// cap it implies is 256 VGPRs per lane, which every instantiation fits without spill
+// (hipcc -Rpass-analysis / .vgpr_count, round 4: 116-247)
 template <int TH, int BN, int WM, int CK, int EP, bool GO>
 __global__ __launch_bounds__(NTB, 2) void conv3_big_kernel(rdn_conv_desc d, int tiles_x, int tiles_y, int nitems) {
   using Cfg = PtCfg<TH, BN, WM, CK>;
