@@ -50,7 +50,7 @@ constexpr int HW_ = TW + 2, HP = (TH + 2) * HW_;
 constexpr int LDS_MAX = 160 * 1024;
 
 #ifndef WG_PIPE
-#define WG_PIPE 3   // B-fragment prefetch depth of the (k-step, n-tile) pipeline; 0: the r03 form
+#define WG_PIPE 0   // B-fragment prefetch depth of the (k-step, n-tile) pipeline; 0: the r03 form
 #endif
 
 template <int BM, int CK>
@@ -60,8 +60,10 @@ struct Geo {
   // 218 VGPRs, 6-8 % faster per launch, profiles/r03_v10_wgrad_glds_diag.txt); the 80-
   // and 96-column groups spilled there, because every k-step's B fragments (NTW of
   // them, double-buffered) were read ahead at once.  Round 4: the (k-step, n-tile)
-  // software pipeline below keeps only WG_PIPE + 1 B fragments live, so every shape
-  // runs two waves per SIMD
+  // software pipeline below (WG_PIPE > 0) keeps only WG_PIPE + 1 B fragments live, so
+  // every shape fits two waves per SIMD -- bit-identical, but 1-6 % slower per launch
+  // on 5 of the 7 train-step shapes and -0.5 % on the step (profiles/r04_v4_wgrad_pipe_*):
+  // kept as the WG_PIPE=n variant, off
   static constexpr int NW = ((WG_PIPE > 0 && BM >= 32 && !(BM == 64 && CK == 96)) || (BM == 64 && CK == 64)) ? 8 : 4,
                        NTH = 64 * NW;   // (64 x 96: 78 VGPRs of spill at two waves per SIMD)
   static constexpr int NCOL = 9 * CK, NT_ALL = (NCOL + 15) / 16;
