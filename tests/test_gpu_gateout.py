@@ -26,7 +26,7 @@ def _grads(gate_out, dtype, B, S, F0=32, seed=0):
     import vub_image_denoising_amd as vm
     from vub_image_denoising_amd import engine as E
     old = E.GATE_OUT
-    E.GATE_OUT = gate_out   # (off by default: engine.py has the step A/B)
+    E.GATE_OUT = gate_out   # (on by default since round 4: engine.py has the step A/B)
     try:
         torch.manual_seed(seed)
         m = vm.RDUNet_T(base_filters=F0).cuda()

@@ -42,7 +42,10 @@ namespace {
 __device__ __attribute__((aligned(64))) unsigned int g_big_zero[16];
 
 #ifndef BIG_PF
-#define BIG_PF 0   // 1: next k-step's fragments read before the current MFMAs (A/B)
+// 1: the next k-step's fragments are read before the current MFMAs (two fragment sets
+// live; bit-identical).  Round 4, interleaved on one box: B16 +0.6 %, B32 +0.5 %
+// (profiles/r04_v5_big_pf_gate_out_ab.txt)
+#define BIG_PF 1
 #endif
 
 template <int N>

@@ -214,12 +214,14 @@ FUSE_DW = os.environ.get("RDN_DW", "1") != "0"
 # PReLU backward of a layer fused into the input-gradient epilogue of its last
 # consumer in backward order (rdn_conv_desc.gout: conv_k+1 finishes dense slice
 # out_k, up_l.conv finishes up_l.conv_t's output), instead of a separate pass.
-# Off by default: per launch it saves 0.5-6 us at levels 2/3 (scripts/gate_kbench.py,
-# profiles/r03_v9_gate_kbench.json), but the whole step measured 1666-1674 img/s
-# with it against 1680-1691 without (8-16 vs 6-12 ring slots, interleaved,
-# profiles/r03_v9_slots_ab.txt): the longer finisher launches sit on the critical path
-# beside the weight-gradient stream.  Tested both ways (tests/test_gpu_gateout.py).
-GATE_OUT = os.environ.get("RDN_GATE_OUT", "0") == "1"
+# Per launch it saves 0.5-6 us at levels 2/3 (scripts/gate_kbench.py,
+# profiles/r03_v9_gate_kbench.json); with the r03 ring of dYpre slots the whole step
+# measured 1666-1674 img/s with it against 1680-1691 without (profiles/r03_v9_slots_ab.txt:
+# the longer finisher launches sat on the critical path beside the weight-gradient
+# stream).  Round 4 (one slot per layer, column-half dw, conv3_big prefetch), interleaved:
+# +0.2 % B16 / +0.2 % B32 on top of the prefetch (profiles/r04_v5_big_pf_gate_out_ab.txt):
+# on by default.  Tested both ways (tests/test_gpu_gateout.py).
+GATE_OUT = os.environ.get("RDN_GATE_OUT", "1") == "1"
 # conv_0..conv_2 of every level-0 DenoisingBlock (base_filters 32, bf16) as ONE
 # launch that reads x once and keeps out_0 / out_1 on chip (rdn_dense3_fwd)
 FUSE_DENSE = os.environ.get("RDN_DENSE", "1") != "0"
