@@ -69,6 +69,9 @@ constexpr int NT = 512;   // 8 waves
 #ifndef DW_SB
 #define DW_SB 1      // one barrier per tile (dY and X halos double-buffered in LDS)
 #endif
+#ifndef DW_DPF
+#define DW_DPF 0     // dgrad: next k-step's fragments read before the current MFMAs (A/B)
+#endif
 constexpr int LDS_MAX = 160 * 1024;
 
 template <int BN, int CK>
@@ -305,23 +308,44 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int jn = 0; jn < NTL; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int j = 0; j < NSTEP; ++j) {
-        int ao;
+      auto aoff_of = [&](int j) {
         if constexpr (KALIGN) {
           const int k0 = 32 * j;
           int tap = k0 / CK;
           const int ci = k0 - tap * CK;
           tap = tap < 9 ? tap : 8;
-          ao = ((tap / 3) * RS + tap % 3) * DROW + ci * 2;
+          return ((tap / 3) * RS + tap % 3) * DROW + ci * 2;
         } else {
-          ao = offA[j];
+          return offA[j];
         }
+      };
+#if DW_DPF
+      // the next k-step's fragments are read before this one's MFMAs (two sets live)
+      u32x4 pa_[2][MT], pb_[2][NTL];
+      auto rdf = [&](int j, int b) {
+        const int ao = aoff_of(j);
+#pragma unroll
+        for (int i = 0; i < MT; ++i) pa_[b][i] = *(const u32x4*)(pda + doff + ao + i * RS * DROW);
+#pragma unroll
+        for (int jn = 0; jn < NTL; ++jn) pb_[b][jn] = *(const u32x4*)(pdb + jn * 16 * WROW + j * 64);
+      };
+      rdf(0, 0);
+#endif
+#pragma unroll
+      for (int j = 0; j < NSTEP; ++j) {
+#if DW_DPF
+        if (j + 1 < NSTEP) rdf(j + 1, (j + 1) & 1);
+        __builtin_amdgcn_sched_barrier(0);
+        const u32x4(&fa)[MT] = pa_[j & 1];
+        const u32x4(&fb)[NTL] = pb_[j & 1];
+#else
+        const int ao = aoff_of(j);
         u32x4 fa[MT], fb[NTL];
 #pragma unroll
         for (int i = 0; i < MT; ++i) fa[i] = *(const u32x4*)(pda + doff + ao + i * RS * DROW);
 #pragma unroll
         for (int jn = 0; jn < NTL; ++jn) fb[jn] = *(const u32x4*)(pdb + jn * 16 * WROW + j * 64);
+#endif
 #pragma unroll
         for (int i = 0; i < MT; ++i)
 #pragma unroll
