@@ -73,8 +73,10 @@ def test_gate_out_bf16_matches_separate(B, S):
     assert torch.equal(y0, y1)
     worst = max(_rel(g1[n], g0[n]) for n in g0)
     assert worst <= 1e-2, sorted(((_rel(g1[n], g0[n]), n) for n in g0), reverse=True)[:5]
-    if S >= 64:   # (64^2: the 8x8 level-3 grids keep the separate pass: no full 8x16 tiles)
-        assert len(k1) >= 16, k1
+    if S >= 64:   # (64^2: the 8x8 level-3 grids keep the separate pass: no full 8x16 tiles;
+        # bf16: level-1 conv_1 / conv_2 run as the fused gated dgrad+wgrad (conv3_dw
+        # column halves), which finishes no other layer -- 14 finishers at 64^2)
+        assert len(k1) >= 14, k1
     if B == 16:   # the train step's shape: conv3_big serves the level-1 and up-conv finishers
         assert any("conv3_big" in k and ",go" in k for _, _, k in k1), k1
         assert any("conv3_halo" in k for _, _, k in k1), k1

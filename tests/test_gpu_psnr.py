@@ -175,6 +175,9 @@ def test_psnr_sigma25_paired_vs_oracle_fixture():
            "psnr_oracle_256": float(np.mean([r["oracle_256"] for r in runs])),
            "gpu_minus_oracle_64": s, "gpu_minus_oracle_256": s256, "inference_parity_db": gpu4 - ora4}
     print("PSNR_PARITY " + json.dumps(res))
+    if os.environ.get("RDN_TEST_OUT"):   # scripts/measure.sh keeps the numbers
+        with open(os.path.join(os.environ["RDN_TEST_OUT"], "psnr_parity.json"), "w") as f:
+            json.dump(res, f, indent=1)
     assert gain >= 3.0 and gain256 > 1.0
     assert abs(gpu4 - ora4) < 1e-4
     for dt in legs:
