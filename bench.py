@@ -477,7 +477,7 @@ def dense_conv_path(prof, batch):
     byts, bmin, ms, n = 0.0, 0.0, 0.0, 0
     for info, s, e in prof.records:
         m = re.match(r"block_(\d)_\d\.conv_[\d-]+$", info[1])   # (conv_0-2: the fused level-0 launch)
-        if m and int(m.group(1)) in DENSE_LEVELS:
+        if m and int(m.group(1)) in DENSE_LEVELS and info[0] != "prelu":   # (convs only)
             byts += info[4]
             bmin += info[5] if len(info) > 5 else info[4]
             ms += s.elapsed_time(e)

@@ -69,7 +69,10 @@ enum {
   RDN_EPI_RESID = 8,     /* v += res[pix, res_c0 + c] for c < res_climit     */
   RDN_EPI_ACCUM = 16,    /* v += out[pix, out_c0 + c] (gradient accumulation) */
   RDN_EPI_SCATTER2 = 32, /* column j = tap*cout + c lands on pixel (2y+dy, 2x+dx) */
-  RDN_EPI_OUT_NCHW = 64  /* write fp32 NCHW out_nchw (residual from res_nchw)  */
+  RDN_EPI_OUT_NCHW = 64, /* write fp32 NCHW out_nchw (residual from res_nchw)  */
+  RDN_EPI_GOUT_KEEP = 128 /* with gout (rdn_conv_dgrad_wgrad only): the gated columns'
+                             dY is stored to out as well (the finished layer's own
+                             residual epilogue reads it)                     */
 };
 
 typedef struct rdn_conv_desc {
@@ -186,6 +189,11 @@ int rdn_conv_dgrad_wgrad_splits(const rdn_conv_desc* dgrad, const rdn_wgrad_desc
    each half with rdn_wgrad_reduce_cols; the dalpha/dbias partials are in half 0's rows,
    half 1's are zero); 0 = not served */
 int rdn_conv_dgrad_wgrad_cols(const rdn_conv_desc* dgrad, const rdn_wgrad_desc* wgrad);
+/* gate-out on the fused pair (dgrad->gout set, as for rdn_conv_fwd; round 4): the
+   shapes of up_0.conv (96 columns in halves) and the level-1 conv_0 (64 columns), no
+   residual, 0 <= gout_c0 < ncols.  Each block writes one partial row (zeros in the
+   columns of the other half): rows = this value (= the split count); 0 = not served */
+int rdn_conv_dgrad_wgrad_gate_rows(const rdn_conv_desc* dgrad, const rdn_wgrad_desc* wgrad);
 /* name of the fused kernel instantiation (1 = not served) */
 int rdn_conv_dgrad_wgrad_kernel_name(const rdn_conv_desc* dgrad, const rdn_wgrad_desc* wgrad, char* buf, int32_t len);
 

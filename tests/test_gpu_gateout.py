@@ -10,7 +10,11 @@ pixel sum is cut into partials (per 8x16 / 16x16 tile instead of per pass block)
 rel-L2 <= 1e-5.  bf16: the gate multiplies the fp32 sum instead of its bf16
 rounding (slope branch: one bf16 rounding fewer), so gradients agree to bf16
 rounding noise: rel-L2 <= 1e-2 per tensor (the full-size oracle tests bound the
-absolute error of the default path)."""
+absolute error of the default path).  bf16 also runs the gate-out epilogue of the
+fused dgrad+wgrad kernel (conv3_dw ",go", round 4): up_0.conv finishing up_0.conv_t
+and the level-1 conv_0s finishing the layer that feeds their block (its residual
+reader, the block's conv_3, adds its share earlier in backward order; a finished
+conv_3 also gets its plain dY stored, RDN_EPI_GOUT_KEEP, for its own residual)."""
 import pytest
 import torch
 
@@ -43,7 +47,8 @@ def _grads(gate_out, dtype, B, S, F0=32, seed=0):
             for eng in pool:
                 for L in eng.layers:
                     if L.extra.get("gates") is not None:
-                        keys.append((L.name, L.extra["gates"].name, L.extra["info"]["dgrad"][2]))
+                        info = L.extra["info"]
+                        keys.append((L.name, L.extra["gates"].name, info["dw"][2] if "dw" in info else info["dgrad"][2]))
         return y.detach().clone(), grads, keys
     finally:
         E.GATE_OUT = old
@@ -77,6 +82,13 @@ def test_gate_out_bf16_matches_separate(B, S):
         # bf16: level-1 conv_1 / conv_2 run as the fused gated dgrad+wgrad (conv3_dw
         # column halves), which finishes no other layer -- 14 finishers at 64^2)
         assert len(k1) >= 14, k1
+    if S >= 64:   # the fused dgrad+wgrad finishers (conv3_dw ",go"): up_0.conv finishes
+        # up_0.conv_t; a level-1 block's conv_0 finishes the layer feeding the block
+        # (encoder block_1_1 <- block_1_0.conv_3; decoder block_1_2 <- up_1.conv,
+        # block_1_3 <- block_1_2.conv_3; block_1_0's input is down_0's, a 2x2 conv: not here)
+        fin = {(j, k) for j, k, key in k1 if key.startswith("conv3_dw") and ",go" in key}
+        assert fin == {("up_0.conv", "up_0.conv_t"), ("block_1_1.conv_0", "block_1_0.conv_3"),
+                       ("block_1_2.conv_0", "up_1.conv"), ("block_1_3.conv_0", "block_1_2.conv_3")}, k1
     if B == 16:   # the train step's shape: conv3_big serves the level-1 and up-conv finishers
         assert any("conv3_big" in k and ",go" in k for _, _, k in k1), k1
         assert any("conv3_halo" in k for _, _, k in k1), k1

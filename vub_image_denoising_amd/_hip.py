@@ -19,6 +19,7 @@ LIB_PATH = os.environ.get("RDN_LIB") or os.path.join(HERE, "librdunet_hip.so")
 RDN_F32, RDN_BF16 = 0, 1
 RDN_G_CONV3, RDN_G_S2, RDN_G_PIX = 0, 1, 2
 EPI_BIAS, EPI_STORE_PRE, EPI_PRELU, EPI_RESID, EPI_ACCUM, EPI_SCATTER2, EPI_OUT_NCHW = 1, 2, 4, 8, 16, 32, 64
+EPI_GOUT_KEEP = 128
 PACK_CONV_FWD, PACK_CONV_DGRAD, PACK_GEMM_T = 0, 1, 2
 
 _vp, _i32, _i64, _f32 = C.c_void_p, C.c_int32, C.c_int64, C.c_float
@@ -85,6 +86,7 @@ SIGNATURES = {
     "rdn_conv_dgrad_wgrad": (_i32, [C.POINTER(ConvDesc), C.POINTER(WgradDesc), _vp]),
     "rdn_conv_dgrad_wgrad_splits": (_i32, [C.POINTER(ConvDesc), C.POINTER(WgradDesc)]),
     "rdn_conv_dgrad_wgrad_cols": (_i32, [C.POINTER(ConvDesc), C.POINTER(WgradDesc)]),
+    "rdn_conv_dgrad_wgrad_gate_rows": (_i32, [C.POINTER(ConvDesc), C.POINTER(WgradDesc)]),
     "rdn_conv_dgrad_wgrad_kernel_name": (_i32, [C.POINTER(ConvDesc), C.POINTER(WgradDesc), C.c_char_p, _i32]),
     "rdn_wgrad_chunks": (_i32, [C.POINTER(WgradDesc)]),
     "rdn_dense3_fwd": (_i32, [C.POINTER(Dense3Desc), _vp]),

@@ -51,6 +51,19 @@
 // (half 1 writes zero rows).  The whole 96 / 128-column tile would not fit: the
 // resident panel and the W waves' accumulators grow with the columns (<96,32>
 // spilled, r02).
+//
+// Gate-out (GO, round 4; d.gout as in conv3_big): when this conv is the last consumer
+// (in backward order) of another layer's output and that output is the tail
+// [gout_c0, ncols) of its input channels, the dX of those channels is that layer's
+// complete dY: the D waves' epilogue gates it with the layer's saved PReLU input
+// (prefetched one tile ahead beside the accumulate operand) and stores its dYpre
+// instead, summing the layer's dalpha / dbias partials in registers; one partial row
+// per block (= per slab; zeros in the columns of the other half); with
+// RDN_EPI_GOUT_KEEP the dY is stored as well (a block's conv_3 reads its own output
+// gradient again as the residual operand of its input gradient).  Served for
+// up_0.conv (finishes up_0.conv_t: <48,32,h2>, gout_c0 = 32) and the level-1
+// conv_0s (finish down_0 / block_1_k.conv_3: <64,32>, gout_c0 = 0), whose separate
+// PReLU-backward passes (73 / 23 us each at B16) leave the compute queue.
 #include "conv3_tile.h"
 
 #include <stdlib.h>
@@ -74,7 +87,7 @@ constexpr int NT = 512;   // 8 waves
 #endif
 constexpr int LDS_MAX = 160 * 1024;
 
-template <int BN, int CK>
+template <int BN, int CK, bool GO = false>
 struct DwCfg {
   static constexpr int KC = (9 * CK + 63) / 64 * 64;   // packed dgrad K (rdn_pack_weights, conv3_ws)
   static constexpr int NSTEP = KC / 32;
@@ -87,6 +100,7 @@ struct DwCfg {
   static constexpr int CT_BYTES = 0;                    // dX leaves from the accumulators
   static constexpr int RED_BYTES = 2 * 256 * 8 * 4;     // dalpha/dbias partial reduction (aliases)
   static constexpr int AL_BYTES = (CK * 4 + 15) / 16 * 16;   // gate slopes
+  static constexpr int GAL_BYTES = GO ? BN * 4 : 0;           // gate-out: the finished layer's slopes
   // W waves keep two X halos in flight in registers where the budget allows it
   // (accumulators MTW x NTW x 4 + two X_IT sets within 256 VGPRs at 2 waves/SIMD);
   // otherwise ONE register set and two X halo buffers in LDS
@@ -99,24 +113,26 @@ struct DwCfg {
   // shapes ran 1-3 us slower and keep two barriers per tile)
   static constexpr bool SB = DW_SB && !((BN == 64 && CK == 16) || (BN == 32 && CK == 32));
   static constexpr int DB = SB ? 2 : 1;
-  static constexpr int BASE = W_BYTES + DB * D_BYTES + CT_BYTES + AL_BYTES;
+  static constexpr int BASE = W_BYTES + DB * D_BYTES + CT_BYTES + AL_BYTES + GAL_BYTES;
   // X halo buffers in LDS: 2 for the LDS double buffer, 1 where it would not fit
   // (96 columns were tried: <96,32> spills 128 B in the W loop, so they stay on the
   // separate kernels)
   static constexpr int XB = SB ? 2 : DW2 ? 1 : (BASE + 2 * X_BYTES <= LDS_MAX ? 2 : 1);
   static constexpr int LDS = BASE + XB * X_BYTES;
-  static constexpr bool FITS = LDS <= LDS_MAX && D_BYTES + X_BYTES + CT_BYTES >= RED_BYTES;
+  static constexpr bool FITS = LDS <= LDS_MAX && D_BYTES + X_BYTES + CT_BYTES >= RED_BYTES &&
+                              (!GO || W_BYTES >= 8 * BN * 4);   // gate-out partials in the dead panel
 };
 
-template <int BN, int CK, int NH>
+template <int BN, int CK, int NH, bool GO>
 __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wgrad_desc wg, int tiles_x, int tiles_y,
                                                          int ntiles) {
-  using Cfg = DwCfg<BN, CK>;
+  using Cfg = DwCfg<BN, CK, GO>;
   constexpr int VEC = 8;
   constexpr int KC = Cfg::KC, NSTEP = Cfg::NSTEP, WROW = Cfg::WROW, DROW = Cfg::DROW, XROW = Cfg::XROW;
   constexpr int NR = 256;                               // threads per role
   constexpr int MT = 2;                                 // dgrad: 2 x 16 pixels per D wave
   constexpr int NTL = BN / 16;                          // dgrad n-tiles
+  constexpr int NE = NTL;                               // epilogue operands per row
   constexpr int DU = CK / VEC, XU = BN / VEC;           // 16-B units per halo pixel
   constexpr int D_UNITS = HW_ * DU, X_UNITS = HW_ * XU;
   constexpr int D_IT = (D_UNITS + NR - 1) / NR, X_IT = (X_UNITS + NR - 1) / NR;
@@ -136,6 +152,8 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
   unsigned char* const dyh = lds + Cfg::W_BYTES;
   unsigned char* const xh = dyh + Cfg::DB * Cfg::D_BYTES;
   float* const alds = (float*)(xh + Cfg::XB * Cfg::X_BYTES + Cfg::CT_BYTES);
+  float* const galds = alds + Cfg::AL_BYTES / 4;        // (GO) slopes of the finished layer, this half's columns
+  float* const gred = (float*)lds;                      // (GO) its partials, [D wave][2][BN] over the dead panel
   float* const red = (float*)(lds + Cfg::W_BYTES);   // partial reduction (aliases the halos after the loops)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -172,6 +190,12 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       *(u32x4*)(wl + n * WROW + k8 * 16) = *(const u32x4*)(WP + (int64_t)(col0 + n) * d.kp + k8 * VEC);
     }
     for (int c = tid; c < CK; c += NT) alds[c] = d.gate_alpha[c];
+    if constexpr (GO) {
+      for (int c = tid; c < BN; c += NT) {
+        const int gc = col0 + c - d.gout_c0;
+        galds[c] = gc >= 0 ? d.gout_alpha[gc] : 0.f;
+      }
+    }
   }
   __syncthreads();   // the gate slopes are read by the first halo store (before the prologue barrier)
 
@@ -224,8 +248,8 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     const bool has_res = flags & RDN_EPI_RESID, has_acc = flags & RDN_EPI_ACCUM;
     const bf16* const ebase = has_res ? (const bf16*)d.res : (const bf16*)d.out;
     const int eps = has_res ? (int)d.res_ps : (int)d.out_ps;
-    int coff_e[NTL], coff_o[NTL];
-    bool eok[NTL];
+    int coff_e[NTL], coff_o[NTL], coff_g[NTL];
+    bool eok[NTL], gon[NTL];
 #pragma unroll
     for (int jn = 0; jn < NTL; ++jn) {
       const int c = col0 + jn * 16 + 4 * g;
@@ -233,7 +257,18 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       coff_e[jn] = has_res ? rdn_coff32(d.res_c0 + c, (int)d.res_ps, (int)d.res_pl)
                            : rdn_coff32(d.out_c0 + c, (int)d.out_ps, (int)d.out_pl);
       coff_o[jn] = rdn_coff32(d.out_c0 + c, (int)d.out_ps, (int)d.out_pl);
+      gon[jn] = GO && c >= d.gout_c0;   // (a 4-channel unit is wholly in or out: gout_c0 % 4 == 0)
+      coff_g[jn] = gon[jn] ? c - d.gout_c0 : 0;
     }
+    // (GO) the finished layer's dalpha / dbias partials of this thread's channels
+    float gsa[GO ? NTL : 1][4], gsb[GO ? NTL : 1][4];
+#pragma unroll
+    for (int jn = 0; jn < (GO ? NTL : 1); ++jn)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        gsa[jn][e] = 0.f;
+        gsb[jn][e] = 0.f;
+      }
     auto load = [&](int tt, u32x4 (&lr)[D_IT], u32x4 (&gr)[D_IT]) {
       int oy, ox, on;
       origin(tt, oy, ox, on);
@@ -273,10 +308,11 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
         *(u32x4*)(dyh + doff + llds[it]) = Unit16<bf16>::pack(dy);
       }
     };
-    auto load_epi = [&](int tt, u32x2 (&eo)[MT][NTL]) {
+    auto load_epi = [&](int tt, u32x2 (&eo)[MT][NE]) {
       int oy, ox, on;
       origin(tt, oy, ox, on);
-      const __amdgpu_buffer_rsrc_t rb = rdn_rsrc(ebase + (((int64_t)on * H + oy) * W + ox) * eps);
+      const int64_t opix0 = ((int64_t)on * H + oy) * W + ox;
+      const __amdgpu_buffer_rsrc_t rb = rdn_rsrc(ebase + opix0 * eps);
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -302,12 +338,27 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     }
     const unsigned char* const pda = dyh + (KALIGN ? a_lane + g * 16 : 0);
     const unsigned char* const pdb = wl + r * WROW + g * 16;
-    auto dgrad_tile = [&](int tt, const u32x2 (&eo)[MT][NTL], int doff) {
+    auto dgrad_tile = [&](int tt, const u32x2 (&eo)[MT][NE], int doff) {
       f32x4 acc[MT][NTL];
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int jn = 0; jn < NTL; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
+      // (GO) the finished layer's PReLU input at the gated units, issued before the
+      // MFMAs (prefetched a tile ahead beside `eo` instead: up_0.conv 227 -> 240 us,
+      // the level-1 conv_0 spilled)
+      u32x2 gp[GO ? MT : 1][GO ? NTL : 1];
+      if constexpr (GO) {
+        int oy, ox, on;
+        origin(tt, oy, ox, on);
+        const __amdgpu_buffer_rsrc_t rp =
+            rdn_rsrc((const bf16*)d.gout_pre + (((int64_t)on * H + oy) * W + ox) * d.gout_pre_ps);
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+          for (int jn = 0; jn < NTL; ++jn)
+            gp[i][jn] = rdn_ld8(rp, gon[jn], (((2 * rw + i) * W + r) * (int)d.gout_pre_ps + coff_g[jn]) * 2);
+      }
       auto aoff_of = [&](int j) {
         if constexpr (KALIGN) {
           const int k0 = 32 * j;
@@ -370,6 +421,25 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
             v[0] += bf16lo(eo[i][jn][0]); v[1] += bf16hi(eo[i][jn][0]);
             v[2] += bf16lo(eo[i][jn][1]); v[3] += bf16hi(eo[i][jn][1]);
           }
+          if constexpr (GO) {
+            if (gon[jn]) {   // complete dY of the finished layer: its dYpre (aten prelu backward)
+              if (flags & RDN_EPI_GOUT_KEEP)   // (and dY itself: that layer's residual epilogue reads it)
+                *(u32x2*)(ob + ((2 * rw + i) * W + r) * (int)d.out_ps + coff_o[jn]) = rdn_pack4(v);
+              const f32x4 al = *(const f32x4*)(galds + jn * 16 + 4 * g);
+              const float pr[4] = {bf16lo(gp[i][jn][0]), bf16hi(gp[i][jn][0]), bf16lo(gp[i][jn][1]),
+                                   bf16hi(gp[i][jn][1])};
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const bool pos = pr[e] > 0.f;
+                if (!pos) gsa[jn][e] += pr[e] * v[e];
+                v[e] = pos ? v[e] : al[e] * v[e];
+                gsb[jn][e] += v[e];
+              }
+              bf16* const gb = (bf16*)d.gout + (((int64_t)on * H + oy) * W + ox) * d.gout_ps;
+              *(u32x2*)(gb + ((2 * rw + i) * W + r) * (int)d.gout_ps + coff_g[jn]) = rdn_pack4(v);
+              continue;
+            }
+          }
 #ifdef DW_DIAG_NO_STORE
           if (flags & (1 << 30))   // never at run time: the values stay live
 #endif
@@ -378,7 +448,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     };
 
     u32x4 lA[D_IT], gA[D_IT], lB[D_IT], gB[D_IT];
-    u32x2 eC[MT][NTL], eN[MT][NTL];
+    u32x2 eC[MT][NE], eN[MT][NE];
     if constexpr (Cfg::SB) {
     // step k computes tile t from buffer k&1 while it gates tile t + per (issued one
     // step earlier) into buffer (k+1)&1 and issues tile t + 2 per: ONE barrier per
@@ -391,7 +461,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       load(min(t + per, t_last), lA, gA);
     }
     __syncthreads();   // weights + first halos
-    auto step = [&](u32x4 (&lc)[D_IT], u32x4 (&gc)[D_IT], const u32x2 (&ec)[MT][NTL], u32x2 (&en)[MT][NTL],
+    auto step = [&](u32x4 (&lc)[D_IT], u32x4 (&gc)[D_IT], const u32x2 (&ec)[MT][NE], u32x2 (&en)[MT][NE],
                     int cur) -> bool {
       const int t1 = t + per;
       store(lc, gc, half == 0 && t1 < t_hi, (cur ^ 1) * Cfg::D_BYTES);   // (past the range: a re-read of the last tile)
@@ -413,7 +483,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     }
     __syncthreads();   // weights + first halos
     auto step = [&](u32x4 (&lc)[D_IT], u32x4 (&gc)[D_IT], u32x4 (&ln)[D_IT], u32x4 (&gn)[D_IT],
-                    const u32x2 (&ec)[MT][NTL], u32x2 (&en)[MT][NTL]) -> bool {
+                    const u32x2 (&ec)[MT][NE], u32x2 (&en)[MT][NE]) -> bool {
       const int t1 = t + per;
       load(min(t + 2 * per, t_last), ln, gn);
       load_epi(min(t1, t_last), en);
@@ -430,6 +500,26 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
 
     // dalpha / dbias partials of this split into LDS (the loop ended with a barrier
     // that both roles passed, so the halo area is free); summed below
+    if constexpr (GO) {   // (the weight panel is dead too: the finished layer's partials)
+#pragma unroll
+      for (int jn = 0; jn < NTL; ++jn)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+#pragma unroll
+          for (int m = 1; m < 16; m <<= 1) {   // over the 16 pixel columns r
+            gsa[jn][e] += __shfl_xor(gsa[jn][e], m, 64);
+            gsb[jn][e] += __shfl_xor(gsb[jn][e], m, 64);
+          }
+      if (r == 0) {
+#pragma unroll
+        for (int jn = 0; jn < NTL; ++jn)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            gred[(rw * 2 + 0) * BN + jn * 16 + 4 * g + e] = gsa[jn][e];
+            gred[(rw * 2 + 1) * BN + jn * 16 + 4 * g + e] = gsb[jn][e];
+          }
+      }
+    }
     if (wg.part) {
 #pragma unroll
       for (int k = 0; k < VEC; ++k) {
@@ -688,6 +778,22 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
         wg.part[((int64_t)slab * 2 + 1) * wg.mdim + rt] = b;
       }
     }
+    if constexpr (GO) {   // the finished layer's row `slab`: this half's columns, zeros elsewhere
+      if (dwave) {
+        const int gcn = d.ncols - d.gout_c0;
+        float* const prt = d.gout_part + (int64_t)slab * 2 * gcn;
+        for (int j = rt; j < gcn; j += NR) {
+          const int cl = d.gout_c0 + j - col0;
+          float a = 0.f, b = 0.f;
+          if (cl >= 0 && cl < BN) {
+            a = (gred[0 * BN + cl] + gred[2 * BN + cl]) + (gred[4 * BN + cl] + gred[6 * BN + cl]);
+            b = (gred[1 * BN + cl] + gred[3 * BN + cl]) + (gred[5 * BN + cl] + gred[7 * BN + cl]);
+          }
+          prt[j] = a;
+          prt[gcn + j] = b;
+        }
+      }
+    }
   }
 }
 
@@ -735,12 +841,26 @@ int dw_nh(const rdn_conv_desc* d) {
   return (dw_halves_enabled() && d->cin == 32 && (d->ncols == 96 || d->ncols == 128)) ? 2 : 1;
 }
 
+// gate-out (d->gout) on this pair: the instantiated shapes (up_0.conv: 96 columns in
+// halves; the level-1 conv_0: 64 columns), whole 4-channel units, 8-byte aligned
+// operands, 32-bit per-tile offsets
+bool dw_gout_ok(const rdn_conv_desc* d, const rdn_wgrad_desc* wg) {
+  const int nh = dw_nh(d);
+  if (d->cin != 32 || !((d->ncols == 96 && nh == 2) || (d->ncols == 64 && nh == 1))) return false;
+  if (!d->gout_pre || !d->gout_alpha || !d->gout_part || !wg->part || (d->flags & RDN_EPI_RESID)) return false;
+  if (d->gout_c0 < 0 || d->gout_c0 >= d->ncols || d->gout_c0 % 4 || d->gout_ps % 4 || d->gout_pre_ps % 4) return false;
+  if (d->gout_ps < d->ncols - d->gout_c0 || d->gout_pre_ps < d->ncols - d->gout_c0) return false;
+  if (((uintptr_t)d->gout & 7) || ((uintptr_t)d->gout_pre & 7) || ((uintptr_t)d->gout_part & 3)) return false;
+  return (int64_t)TH * d->w * d->gout_ps < (1ll << 30) && (int64_t)TH * d->w * d->gout_pre_ps < (1ll << 30);
+}
+
 // the pair this kernel serves (else 1 = run the separate dgrad / wgrad launches)
 bool dw_serves(const rdn_conv_desc* d, const rdn_wgrad_desc* wg) {
   if (!dw_enabled() || !d || !wg) return false;
   if (d->dtype != RDN_BF16 || wg->dtype != RDN_BF16 || d->gather != RDN_G_CONV3 || wg->gather != RDN_G_CONV3) return false;
-  if (!d->gate || !wg->a_gate || !d->gate_alpha || d->bn || d->bm || d->gout) return false;
-  if (d->flags & ~(RDN_EPI_RESID | RDN_EPI_ACCUM)) return false;
+  if (!d->gate || !wg->a_gate || !d->gate_alpha || d->bn || d->bm) return false;
+  if (d->gout && !dw_gout_ok(d, wg)) return false;
+  if (d->flags & ~(RDN_EPI_RESID | RDN_EPI_ACCUM | (d->gout ? RDN_EPI_GOUT_KEEP : 0))) return false;
   if ((d->flags & RDN_EPI_RESID) && (d->flags & RDN_EPI_ACCUM)) return false;
   if (d->h % TH || d->w % TW || d->n != wg->n || d->h != wg->h || d->w != wg->w) return false;
   if (d->cin != 16 && d->cin != 32) return false;
@@ -771,29 +891,36 @@ bool dw_serves(const rdn_conv_desc* d, const rdn_wgrad_desc* wg) {
   return nt < (1ll << 31);
 }
 
-template <int BN, int CK, int NH = 1>
+template <int BN, int CK, int NH = 1, bool GO = false>
 int launch_dw(const rdn_conv_desc* d, const rdn_wgrad_desc* wg, hipStream_t st) {
-  if constexpr (!DwCfg<BN, CK>::FITS) {
+  if constexpr (!DwCfg<BN, CK, GO>::FITS) {
     return 1;
   } else {
     const int tiles_x = d->w / TW, tiles_y = d->h / TH;
     const int ntiles = d->n * tiles_x * tiles_y;
     const int grid = dw_grid(ntiles, NH);
-    if (NH > 1) RDN_PROBE("conv3_dw_kernel<bf16,%d,%d,h%d>", BN, CK, NH);
-    RDN_PROBE("conv3_dw_kernel<bf16,%d,%d>", BN, CK);
+    if (NH > 1) RDN_PROBE("conv3_dw_kernel<bf16,%d,%d,h%d%s>", BN, CK, NH, GO ? ",go" : "");
+    RDN_PROBE("conv3_dw_kernel<bf16,%d,%d%s>", BN, CK, GO ? ",go" : "");
     if (wg->splits != grid) {
       rdn_set_error("rdn_conv_dgrad_wgrad: wgrad splits %d != %d (rdn_conv_dgrad_wgrad_splits)", wg->splits, grid);
       return RDN_E_ARG;
     }
     if (!wg->ws) { rdn_set_error("rdn_conv_dgrad_wgrad: null workspace"); return RDN_E_ARG; }
-    hipLaunchKernelGGL((conv3_dw_kernel<BN, CK, NH>), dim3((unsigned)grid), dim3(NT), 0, st, *d, *wg, tiles_x, tiles_y,
-                       ntiles);
+    hipLaunchKernelGGL((conv3_dw_kernel<BN, CK, NH, GO>), dim3((unsigned)grid), dim3(NT), 0, st, *d, *wg, tiles_x,
+                       tiles_y, ntiles);
     return rdn_check_launch("rdn_conv_dgrad_wgrad");
   }
 }
 
 template <int CK>
 int dw_bn(const rdn_conv_desc* d, const rdn_wgrad_desc* wg, hipStream_t st) {
+  if (d->gout) {   // (dw_gout_ok: these two shapes only)
+    if constexpr (CK == 32) {
+      if (d->ncols == 96) return launch_dw<48, 32, 2, true>(d, wg, st);
+      if (d->ncols == 64) return launch_dw<64, 32, 1, true>(d, wg, st);
+    }
+    return 1;
+  }
   if constexpr (CK == 32) {
     if (dw_nh(d) == 2) {
       switch (d->ncols) {
@@ -844,6 +971,13 @@ extern "C" int rdn_conv_dgrad_wgrad_splits(const rdn_conv_desc* dgrad, const rdn
 extern "C" int rdn_conv_dgrad_wgrad_cols(const rdn_conv_desc* dgrad, const rdn_wgrad_desc* wgrad) {
   if (!rdn_conv_dgrad_wgrad_splits(dgrad, wgrad)) return 0;
   return dgrad->ncols / dw_nh(dgrad);
+}
+
+// partial rows the gate-out epilogue writes for the finished layer (one per block of
+// the persistent grid = the split count), 0 if this pair with its d->gout is not served
+extern "C" int rdn_conv_dgrad_wgrad_gate_rows(const rdn_conv_desc* dgrad, const rdn_wgrad_desc* wgrad) {
+  if (!dgrad || !wgrad || !dgrad->gout) return 0;
+  return rdn_conv_dgrad_wgrad_splits(dgrad, wgrad);
 }
 
 extern "C" int rdn_conv_dgrad_wgrad_kernel_name(const rdn_conv_desc* dgrad, const rdn_wgrad_desc* wgrad, char* buf,

@@ -222,6 +222,9 @@ FUSE_DW = os.environ.get("RDN_DW", "1") != "0"
 # +0.2 % B16 / +0.2 % B32 on top of the prefetch (profiles/r04_v5_big_pf_gate_out_ab.txt):
 # on by default.  Tested both ways (tests/test_gpu_gateout.py).
 GATE_OUT = os.environ.get("RDN_GATE_OUT", "1") == "1"
+# gate-out in the fused dgrad+wgrad kernel (conv3_dw ",go": up_0.conv finishing
+# up_0.conv_t, the level-1 conv_0s finishing down_0 / the previous block's conv_3)
+GATE_OUT_DW = os.environ.get("RDN_GATE_OUT_DW", "1") == "1"
 # conv_0..conv_2 of every level-0 DenoisingBlock (base_filters 32, bf16) as ONE
 # launch that reads x once and keeps out_0 / out_1 on chip (rdn_dense3_fwd)
 FUSE_DENSE = os.environ.get("RDN_DENSE", "1") != "0"
@@ -916,21 +919,28 @@ class UNetEngine:
         lib = H.lib()
         index = {id(L): i for i, L in enumerate(self.layers)}
         for K in self.layers:
-            # (level 0: the finisher's 8-byte-per-lane epilogue streams the extra PReLU
-            # input slower than the separate pass does -- up_0: +13 us per step)
-            if (K.extra["fused"] or K.dst is None or K.kind == "down" or K.cout != K.cout_pad
-                    or self._out_level(K) == 0):
+            if K.extra["fused"] or K.dst is None or K.kind == "down" or K.cout != K.cout_pad:
                 continue
             lo, hi = K.dst.c0, K.dst.c0 + K.cout
             cons = [L for L in self.layers if index[id(L)] > index[id(K)] and L.src.buf == K.dst.buf
                     and L.src.c0 < hi and L.src.c0 + L.cin > lo]
-            # a residual reader of the slice adds its gradient in another epilogue: not here
-            resid = any(L.resid is not None and L.resid.buf == K.dst.buf and L.resid.c0 < hi
-                        and L.resid.c0 + L.resid_c > lo for L in self.layers)
-            if not cons or resid:
+            if not cons:
                 continue
             J = min(cons, key=lambda L: index[id(L)])   # last in backward order
-            if (J.kind != "c3" or J.extra["dw"] or J.extra.get("gates") is not None or J.src.buf in self.pure_inputs
+            dwj = bool(J.extra["dw"])
+            # a residual reader of the slice adds its gradient in its own dgrad epilogue;
+            # the fused dgrad+wgrad finisher runs after every such reader in backward
+            # order (the next block's conv_3 before its conv_0), the others never do
+            resid = [L for L in self.layers if L.resid is not None and L.resid.buf == K.dst.buf and
+                     L.resid.c0 < hi and L.resid.c0 + L.resid_c > lo]
+            if resid and not (dwj and all(index[id(L)] > index[id(J)] for L in resid)):
+                continue
+            # (level 0 with a conv3_big / conv3_halo finisher: its 8-byte-per-lane epilogue
+            # streamed the extra PReLU input slower than the separate pass -- up_0: +13 us
+            # per step; the fused dgrad+wgrad finisher prefetches it with the dX operand)
+            if self._out_level(K) == 0 and not dwj:
+                continue
+            if (J.kind != "c3" or J.extra.get("gates") is not None or J.src.buf in self.pure_inputs
                     or J.cin != J.cin_pad or J.src.c0 + J.cin != hi or J.src.c0 > lo):
                 continue
             pre = self.bufs[K.pre]
@@ -940,8 +950,15 @@ class UNetEngine:
             d.gout_alpha = self.named[K.act + ".weight"].data_ptr()
             d.gout_part = 4096   # stand-in until the workspace exists (rows probe)
             d.gout_c0 = lo - J.src.c0
-            rows = lib.rdn_conv_gate_rows(C.byref(d))
+            if dwj:   # one partial row per block of the fused kernel's persistent grid
+                if K.resid is not None:   # K's own dgrad reads its dY again (residual operand)
+                    d.flags |= H.EPI_GOUT_KEEP
+                wq = self._probe_copy(J.wgrad_desc, H.WgradDesc, ("a_gate", "a_gate_alpha"))   # (part: stand-in)
+                rows = lib.rdn_conv_dgrad_wgrad_gate_rows(C.byref(d), C.byref(wq)) if GATE_OUT_DW else 0
+            else:
+                rows = lib.rdn_conv_gate_rows(C.byref(d))
             if rows <= 0:
+                d.flags &= ~H.EPI_GOUT_KEEP
                 d.gout = d.gout_pre = d.gout_alpha = d.gout_part = None
                 d.gout_ps = d.gout_pre_ps = d.gout_c0 = 0
                 continue
@@ -1005,11 +1022,18 @@ class UNetEngine:
                 # PReLU input of the output slice
                 gate = Pout * L.cout if L.extra.get("fused") else 0
                 gout = Pin * L.extra["gates"].cout if L.extra.get("gates") is not None else 0
+                if L.dgrad_desc.flags & H.EPI_GOUT_KEEP:   # (dY stored beside its dYpre)
+                    gout *= 2
                 dg_bytes = es * (Pout * L.cout + gate + Pin * L.cin * (2 if L.accum else 1) + gout +
                                  (Pin * L.resid_c if L.resid is not None else 0))
-                info["dgrad"] = ("dgrad", L.name, self._kernel_key(L.dgrad_desc), 2 * macs, dg_bytes)
+                # (a fused layer's dgrad descriptor is the fused kernel's: no separate key)
+                dkey = "conv3_dw_kernel" if L.extra.get("dw") else self._kernel_key(L.dgrad_desc)
+                info["dgrad"] = ("dgrad", L.name, dkey, 2 * macs, dg_bytes)
                 info["wgrad"] = ("wgrad", L.name, self._wgrad_key(L.wgrad_desc), 2 * macs,
                                  es * (Pout * L.cout + gate + Pin * L.cin))
+                if not (L.extra.get("fused") or "gated_by" in L.extra):
+                    # the separate PReLU-backward pass: dY + PReLU input read, dYpre written
+                    info["prelu"] = ("prelu", L.name, "prelu_bwd_kernel", 0, 3 * es * Pout * L.cout)
                 if L.extra.get("dw"):   # one pass: dY + gate + X read once, dX written
                     info["dw"] = ("dwgrad", L.name, self._dw_key(L.dgrad_desc, L.wgrad_desc), 4 * macs,
                                   dg_bytes + es * Pin * L.cin)
@@ -1132,14 +1156,18 @@ class UNetEngine:
                 if side is not None and b >= self.slots:
                     main.wait_event(rev[b - self.slots].extra["ev_done"])
                 if L.ddst is None:
+                    tok = tr.start(info["prelu"]) if tr is not None else None
                     rc = lib.rdn_prelu_bwd(self.code, P, n, h, w, L.cout, L.cout_pad, None, 0, 0, 0, dy.data_ptr(),
                                            pre.data_ptr(), pre.shape[1], self.named[L.act + ".weight"].data_ptr(),
                                            dyp, None, None, pws, st)
                 else:
                     dd_ptr, dd_ps, dd_c0, dd_pl = self._slice(L.ddst)
+                    tok = tr.start(info["prelu"]) if tr is not None else None
                     rc = lib.rdn_prelu_bwd(self.code, P, n, h, w, L.cout, L.cout_pad, dd_ptr, dd_ps,
                                            dd_c0, dd_pl, None, pre.data_ptr(), pre.shape[1],
                                            self.named[L.act + ".weight"].data_ptr(), dyp, None, None, pws, st)
+                if tok is not None:
+                    tr.stop(tok)
             if rc:
                 H.check(rc, f"prelu_bwd[{L.name}]")
             dw = L.extra["dw"]
@@ -1149,6 +1177,10 @@ class UNetEngine:
                 # reduced the layer that used the slot before
                 if side is not None and b >= self.slots:
                     main.wait_event(rev[b - self.slots].extra["ev_done"])
+                K = L.extra.get("gates")
+                if K is not None and side is not None and K.extra["bidx"] >= self.slots:
+                    # (gate-out) this epilogue writes K's dYpre / partials into K's ring slot
+                    main.wait_event(rev[K.extra["bidx"] - self.slots].extra["ev_done"])
                 tok = tr.start(info["dw"]) if tr is not None else None
                 rc = lib.rdn_conv_dgrad_wgrad(C.byref(L.dgrad_desc), C.byref(L.wgrad_desc), st)
                 if tok is not None:
