@@ -213,6 +213,9 @@ typedef struct rdn_dense3_desc {
   const float* bias[3]; const float* alpha[3];
 } rdn_dense3_desc;
 int rdn_dense3_fwd(const rdn_dense3_desc* d, void* stream);
+/* name of the instantiation (tile geometry: 8x16, 16x16 or 8x32 output pixels, env
+   RDN_DENSE_TILE) rdn_dense3_fwd launches for d; nothing is launched */
+int rdn_dense3_kernel_name(const rdn_dense3_desc* d, char* buf, int32_t len);
 
 /* PReLU backward (+ conv bias gradient) over a pixel grid of `pixels` pixels:
    dyp[p, c] = dy[p, c] * (pre[p, c] > 0 ? 1 : alpha[c])   (c < C; 0 for C <= c < cpad)

@@ -5,7 +5,8 @@ replaces.  The fused kernel multiplies the same bf16 operands in the same k orde
 before conv_1 / conv_2 read them, exactly as the HBM round trip does, so the network
 output, every saved PReLU input and therefore every gradient are bit-identical.
 Shapes: the train step's 256^2, a small image whose tiles all touch the border, and a
-non-square one."""
+non-square one; the 256-pixel-tile geometries (16 x 16, 8 x 32, round 4) at 256^2 and
+on a non-square 128 x 160 image, each selected by RDN_DENSE_TILE (read per launch)."""
 import pytest
 import torch
 
@@ -29,18 +30,25 @@ def _run(fuse, B, Hh, Ww, seed=0):
         (y * w).mean().backward()
         grads = {n: p.grad.detach().clone() for n, p in m.named_parameters()}
         fused = sum("dense3" in L.extra for pool in m._rdn_engines.values() for eng in pool for L in eng.layers)
+        keys = {L.extra["info"]["dense3"][2] for pool in m._rdn_engines.values() for eng in pool for L in eng.layers
+                if L.extra.get("info", {}).get("dense3")}
         with torch.no_grad():   # inference engine (no PReLU inputs kept)
             y_inf = m(x, t)
-        return y.detach().clone(), y_inf, grads, fused
+        return y.detach().clone(), y_inf, grads, fused, keys
     finally:
         E.FUSE_DENSE = old
 
 
-@pytest.mark.parametrize("B,Hh,Ww", [(2, 256, 256), (1, 64, 64), (2, 40, 48)])
-def test_dense3_bit_identical(B, Hh, Ww):
-    y0, yi0, g0, n0 = _run(False, B, Hh, Ww)
-    y1, yi1, g1, n1 = _run(True, B, Hh, Ww)
+@pytest.mark.parametrize("B,Hh,Ww,tile", [(2, 256, 256, "8x32"), (2, 256, 256, "16x16"), (2, 256, 256, "8x16"),
+                                          (4, 128, 160, "8x32"), (4, 128, 160, "16x16"), (1, 64, 64, None),
+                                          (2, 40, 48, None)])
+def test_dense3_bit_identical(B, Hh, Ww, tile, monkeypatch):
+    if tile is not None:
+        monkeypatch.setenv("RDN_DENSE_TILE", tile)
+    y0, yi0, g0, n0, _ = _run(False, B, Hh, Ww)
+    y1, yi1, g1, n1, k1 = _run(True, B, Hh, Ww)
     assert n0 == 0 and n1 == 4, (n0, n1)
+    assert k1 == {f"conv3_dense_kernel<bf16,32,16,{tile or '8x16'}>"}, k1
     assert torch.equal(y0, y1)
     assert torch.equal(yi0, yi1)
     for n in g0:

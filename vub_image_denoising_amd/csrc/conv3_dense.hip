@@ -32,19 +32,34 @@
 // registers while the current tile computes.
 #include "rdn_common.h"
 
+#include <cstdlib>
+#include <cstring>
+
 namespace {
 
 constexpr int NW = 8, NT = 64 * NW;   // two waves per SIMD
-constexpr int TH = 8, TW = 16;
-constexpr int RW = TW + 6, RH = TH + 6;        // the x region (3-pixel halo)
 // C row pitch (bytes): 128 + 32.  ds_read_b128 serves 64 lanes in four 16-lane groups
 // that mix pixel rows r and k units g; checked over every k step and m-tile of the
 // three convs, 144-B rows conflicted 2.6 / 2.6 / 2.0-way on average, 160-B rows
 // 1.6 / 1.7 / 1.0 (the rest: output-region row breaks)
 constexpr int CP = 160;
-constexpr int C_BYTES = RH * RW * CP;
-constexpr int NXU = RH * RW * 4;               // 16-B units of x in the region
-constexpr int X_IT = (NXU + NT - 1) / NT;
+
+// Tile geometry (round 4: TH x TW = 16 x 32 where the image divides, else 8 x 16).
+// The halo recompute per output pixel: conv_0 on (TH+4)(TW+4), conv_1 on (TH+2)(TW+2),
+// in m-tiles of 16 region pixels padded to a multiple of the 8 waves: 4.0 MFMA
+// slot-steps per pixel at 8 x 16, 3.06 at 16 x 32 (every B fragment is one LDS read:
+// the convs' 16 output channels give each pixel fragment a single MFMA), and the x
+// halo read 2.41 -> 1.63 times per pixel.
+template <int TH_, int TW_>
+struct DGeo {
+  static constexpr int TH = TH_, TW = TW_;
+  static constexpr int RW = TW + 6, RH = TH + 6;        // the x region (3-pixel halo)
+  static constexpr int C_BYTES = RH * RW * CP;
+  static constexpr int NXU = RH * RW * 4;               // 16-B units of x in the region
+  static constexpr int X_IT = (NXU + NT - 1) / NT;
+  static constexpr int mt(int npx) { return ((npx + 15) / 16 + NW - 1) / NW * NW; }
+  static constexpr int NMT0 = mt((TH + 4) * (TW + 4)), NMT1 = mt((TH + 2) * (TW + 2)), NMT2 = mt(TH * TW);
+};
 
 template <int CIN> struct WCfg {
   static constexpr int K = 9 * CIN, NSTEP = (K + 31) / 32, KC = (K + 63) / 64 * 64;
@@ -54,8 +69,6 @@ template <int CIN> struct WCfg {
 using W0 = WCfg<32>;
 using W1 = WCfg<48>;
 using W2 = WCfg<64>;
-constexpr int W2_OFF = C_BYTES;                 // conv_2's weights: LDS (registers: conv_0, conv_1)
-constexpr int LDS_BYTES = W2_OFF + W2::BYTES;
 
 struct Out { __amdgpu_buffer_rsrc_t o, p; };
 
@@ -73,10 +86,11 @@ __device__ __forceinline__ void bar_lds() {
 // of 16 output-region pixels, MTW = NMT / NW per wave (m-tile wave + NW i); the
 // weights are this lane's A fragments, resident in registers (wreg[j]: row r,
 // k = 32 j + 8 g .. +7)
-template <int CIN, int HO, int NMT, bool WREG>
+template <class G, int CIN, int HO, int NMT, bool WREG>
 __device__ __forceinline__ void dense_conv(const unsigned char* __restrict__ lds, int wave, int r, int g,
                                            const u32x4* wreg, const unsigned char* __restrict__ wimg,
                                            f32x4 (&acc)[NMT / NW]) {
+  constexpr int TH = G::TH, TW = G::TW, RW = G::RW;
   using WC = WCfg<CIN>;
   constexpr int MTW = NMT / NW;
   constexpr int OW = TW + 2 * HO;                      // output region width
@@ -116,10 +130,11 @@ __device__ __forceinline__ void dense_conv(const unsigned char* __restrict__ lds
 
 // epilogue of conv k: bias, PReLU input (tile pixels), PReLU, output (tile pixels) and,
 // for k < 2, the bf16 copy in C (channels 32 + 16k.., zero outside the image)
-template <int HO, int NMT, int KIDX>
+template <class G, int HO, int NMT, int KIDX>
 __device__ __forceinline__ void dense_epi(unsigned char* __restrict__ lds, int wave, int r, int g, const f32x4 (&acc)[NMT / NW],
                                           const f32x4& bias, const f32x4& alpha, const Out& o, int y0, int x0, int H,
                                           int W) {
+  constexpr int TH = G::TH, TW = G::TW, RW = G::RW;
   constexpr int MTW = NMT / NW;
   constexpr int OW = TW + 2 * HO;
   constexpr int NPX = (TH + 2 * HO) * OW;
@@ -154,8 +169,13 @@ __device__ __forceinline__ void dense_epi(unsigned char* __restrict__ lds, int w
   }
 }
 
+template <int TH, int TW>
 __global__ __launch_bounds__(NT, 1) void conv3_dense_kernel(rdn_dense3_desc d, int tiles_x, int tiles_y, int ntiles) {
-  __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
+  using G = DGeo<TH, TW>;
+  constexpr int RW = G::RW, X_IT = G::X_IT, NXU = G::NXU;
+  constexpr int W2_OFF = G::C_BYTES;              // conv_2's weights: LDS (registers: conv_0, conv_1)
+  static_assert(W2_OFF + W2::BYTES <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) unsigned char lds[W2_OFF + W2::BYTES];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int H = d.h, W = d.w;
@@ -195,16 +215,16 @@ __global__ __launch_bounds__(NT, 1) void conv3_dense_kernel(rdn_dense3_desc d, i
 
   // ---- x region loads: unit u -> region pixel u / 4, x channels 8 (u % 4) ..; the
   // two 16-channel planes of the block buffer (channel-blocked, 32-byte pixel rows)
-  int xrel[X_IT], xlds[X_IT], xhy[X_IT], xhx[X_IT];
-#pragma unroll
-  for (int it = 0; it < X_IT; ++it) {
+  // (unit it of this thread: recomputed per use -- four index arrays of X_IT registers
+  // each spilled the 16 x 32 geometry)
+  auto xunit = [&](int it, int& hy, int& hx, int& rel, int& lo) {
     const int u = tid + it * NT;
     const int hp = u < NXU ? u / 4 : 0, cu = u & 3;
-    xhy[it] = hp / RW;
-    xhx[it] = hp - xhy[it] * RW;
-    xrel[it] = (cu >> 1) * (int)d.x_pl + (xhy[it] * W + xhx[it]) * 16 + (cu & 1) * 8;
-    xlds[it] = u < NXU ? hp * CP + cu * 16 : -1;
-  }
+    hy = hp / RW;
+    hx = hp - hy * RW;
+    rel = (cu >> 1) * (int)d.x_pl + (hy * W + hx) * 16 + (cu & 1) * 8;
+    lo = u < NXU ? hp * CP + cu * 16 : -1;
+  };
   u32x4 xr[X_IT];
   auto load_x = [&](int tt) {
     const int tx = tt % tiles_x, t1 = tt / tiles_x;
@@ -212,15 +232,19 @@ __global__ __launch_bounds__(NT, 1) void conv3_dense_kernel(rdn_dense3_desc d, i
     const __amdgpu_buffer_rsrc_t rx = rdn_rsrc((const bf16*)d.x + (((int64_t)nimg * H + (y0 - 3)) * W + (x0 - 3)) * 16);
 #pragma unroll
     for (int it = 0; it < X_IT; ++it) {
-      const bool ok = xlds[it] >= 0 && (unsigned)(y0 - 3 + xhy[it]) < (unsigned)H &&
-                      (unsigned)(x0 - 3 + xhx[it]) < (unsigned)W;
-      xr[it] = rdn_ld16(rx, ok, xrel[it] * 2);
+      int hy, hx, rel, lo;
+      xunit(it, hy, hx, rel, lo);
+      const bool ok = lo >= 0 && (unsigned)(y0 - 3 + hy) < (unsigned)H && (unsigned)(x0 - 3 + hx) < (unsigned)W;
+      xr[it] = rdn_ld16(rx, ok, rel * 2);
     }
   };
   auto store_x = [&]() {
 #pragma unroll
-    for (int it = 0; it < X_IT; ++it)
-      if (xlds[it] >= 0) *(u32x4*)(lds + xlds[it]) = xr[it];
+    for (int it = 0; it < X_IT; ++it) {
+      int hy, hx, rel, lo;
+      xunit(it, hy, hx, rel, lo);
+      if (lo >= 0) *(u32x4*)(lds + lo) = xr[it];
+    }
   };
 
   load_x(t);
@@ -239,21 +263,21 @@ __global__ __launch_bounds__(NT, 1) void conv3_dense_kernel(rdn_dense3_desc d, i
       o[k].p = rdn_rsrc((const bf16*)d.pre[k] + pix0 * 16);
     }
     {
-      f32x4 acc[2];
-      dense_conv<32, 2, 16, true>(lds, wave, r, g, w0, nullptr, acc);
-      dense_epi<2, 16, 0>(lds, wave, r, g, acc, bias[0], alpha[0], o[0], y0, x0, H, W);
+      f32x4 acc[G::NMT0 / NW];
+      dense_conv<G, 32, 2, G::NMT0, true>(lds, wave, r, g, w0, nullptr, acc);
+      dense_epi<G, 2, G::NMT0, 0>(lds, wave, r, g, acc, bias[0], alpha[0], o[0], y0, x0, H, W);
     }
     bar_lds();
     {
-      f32x4 acc[2];   // 12 m-tiles padded to 16: every wave two (the critical path either way)
-      dense_conv<48, 1, 16, true>(lds, wave, r, g, w1, nullptr, acc);
-      dense_epi<1, 16, 1>(lds, wave, r, g, acc, bias[1], alpha[1], o[1], y0, x0, H, W);
+      f32x4 acc[G::NMT1 / NW];   // (8 x 16: 12 m-tiles padded to 16, the critical path either way)
+      dense_conv<G, 48, 1, G::NMT1, true>(lds, wave, r, g, w1, nullptr, acc);
+      dense_epi<G, 1, G::NMT1, 1>(lds, wave, r, g, acc, bias[1], alpha[1], o[1], y0, x0, H, W);
     }
     bar_lds();
     {
-      f32x4 acc[1];
-      dense_conv<64, 0, 8, false>(lds, wave, r, g, nullptr, lds + W2_OFF, acc);
-      dense_epi<0, 8, 2>(lds, wave, r, g, acc, bias[2], alpha[2], o[2], y0, x0, H, W);
+      f32x4 acc[G::NMT2 / NW];
+      dense_conv<G, 64, 0, G::NMT2, false>(lds, wave, r, g, nullptr, lds + W2_OFF, acc);
+      dense_epi<G, 0, G::NMT2, 2>(lds, wave, r, g, acc, bias[2], alpha[2], o[2], y0, x0, H, W);
     }
     bar_lds();   // C's x rows are free (the compiler's own vmcnt wait before store_x
                  // counts the epilogue stores issued after the x loads)
@@ -263,6 +287,36 @@ __global__ __launch_bounds__(NT, 1) void conv3_dense_kernel(rdn_dense3_desc d, i
     }
     t = nxt;
   }
+}
+
+// tile geometry: RDN_DENSE_TILE = 8x16 (round 3) | 16x16 | 8x32 (read per launch: the
+// GPU test runs every geometry); 16 x 32 spilled 156 B/lane at 256 VGPRs
+int dense_tile() {
+  const char* e = getenv("RDN_DENSE_TILE");
+  if (e && !strcmp(e, "8x16")) return 0;
+  if (e && !strcmp(e, "16x16")) return 1;
+  return 2;
+}
+
+template <int TH, int TW>
+int launch_dense(const rdn_dense3_desc* d, hipStream_t st) {
+  const int tiles_x = d->w / TW, tiles_y = d->h / TH;
+  const int64_t ntiles = (int64_t)d->n * tiles_x * tiles_y;
+  if (ntiles >= (1ll << 31)) { rdn_set_error("rdn_dense3_fwd: too many tiles"); return RDN_E_SHAPE; }
+  // 32-bit buffer offsets from a tile's origin (x: plane 1 + 3-pixel halo rows)
+  if (2 * (d->x_pl + (int64_t)(TH + 7) * d->w * 16) >= (int64_t)RDN_OOB - 64) {
+    rdn_set_error("rdn_dense3_fwd: planes too far apart for 32-bit offsets");
+    return RDN_E_SHAPE;
+  }
+  RDN_PROBE("conv3_dense_kernel<bf16,32,16,%dx%d>", TH, TW);
+  int dev = 0, cus = 0;
+  (void)hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 8) cus = 256;
+  int64_t per_xcd = (ntiles + 7) / 8;
+  int slots = cus / 8;
+  if (slots > per_xcd) slots = (int)per_xcd;
+  conv3_dense_kernel<TH, TW><<<8 * slots, NT, 0, st>>>(*d, tiles_x, tiles_y, (int)ntiles);
+  return rdn_check_launch("rdn_dense3_fwd");
 }
 
 }  // namespace
@@ -279,25 +333,27 @@ extern "C" int rdn_dense3_fwd(const rdn_dense3_desc* d, void* stream) {
     rdn_set_error("rdn_dense3_fwd: packed K too small (pack with ck = cin)");
     return RDN_E_SHAPE;
   }
-  if (d->n <= 0 || d->h % TH || d->w % TW || ((uintptr_t)d->x & 15) || d->x_pl < (int64_t)d->n * d->h * d->w * 16) {
+  if (d->n <= 0 || d->h % 8 || d->w % 16 || ((uintptr_t)d->x & 15) || d->x_pl < (int64_t)d->n * d->h * d->w * 16) {
     rdn_set_error("rdn_dense3_fwd: needs H %% 8 == 0, W %% 16 == 0 and a channel-blocked x (16-channel planes)");
     return RDN_E_SHAPE;
   }
-  // 32-bit buffer offsets from a tile's origin (x: plane 1 + 3-pixel halo rows)
-  if (2 * (d->x_pl + (int64_t)(TH + 7) * d->w * 16) >= (int64_t)RDN_OOB - 64) {
-    rdn_set_error("rdn_dense3_fwd: planes too far apart for 32-bit offsets");
-    return RDN_E_SHAPE;
-  }
-  const int tiles_x = d->w / TW, tiles_y = d->h / TH;
-  const int64_t ntiles = (int64_t)d->n * tiles_x * tiles_y;
-  if (ntiles >= (1ll << 31)) { rdn_set_error("rdn_dense3_fwd: too many tiles"); return RDN_E_SHAPE; }
-  RDN_PROBE("conv3_dense_kernel<bf16,32,16>");
-  int dev = 0, cus = 0;
-  (void)hipGetDevice(&dev);
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 8) cus = 256;
-  int64_t per_xcd = (ntiles + 7) / 8;
-  int slots = cus / 8;
-  if (slots > per_xcd) slots = (int)per_xcd;
-  conv3_dense_kernel<<<8 * slots, NT, 0, (hipStream_t)stream>>>(*d, tiles_x, tiles_y, (int)ntiles);
-  return rdn_check_launch("rdn_dense3_fwd");
+  // (256-pixel tiles: at least one tile per CU, else the 8 x 16 grid fills the chip better)
+  const int tile = dense_tile();
+  const int64_t px = (int64_t)d->n * d->h * d->w;
+  if (tile == 1 && d->h % 16 == 0 && d->w % 16 == 0 && px >= 256ll * 256)
+    return launch_dense<16, 16>(d, (hipStream_t)stream);
+  if (tile == 2 && d->w % 32 == 0 && px >= 256ll * 256)
+    return launch_dense<8, 32>(d, (hipStream_t)stream);
+  return launch_dense<8, 16>(d, (hipStream_t)stream);
+}
+
+// name of the instantiation (tile geometry) rdn_dense3_fwd would launch for d
+extern "C" int rdn_dense3_kernel_name(const rdn_dense3_desc* d, char* buf, int32_t len) {
+  if (!buf || len < 1) { rdn_set_error("rdn_dense3_kernel_name: no buffer"); return RDN_E_ARG; }
+  buf[0] = 0;
+  rdn_probe_buf = buf;
+  rdn_probe_len = len;
+  const int rc = rdn_dense3_fwd(d, nullptr);
+  rdn_probe_buf = nullptr;
+  return rc;
 }

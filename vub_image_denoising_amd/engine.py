@@ -992,6 +992,13 @@ class UNetEngine:
         H.check(H.lib().rdn_wgrad_kernel_name(C.byref(d), buf, 128), "rdn_wgrad_kernel_name")
         return buf.value.decode()
 
+    @staticmethod
+    def _dense3_key(d3):
+        """Kernel instantiation (tile geometry) the fused conv_0..2 launch takes."""
+        buf = C.create_string_buffer(128)
+        H.check(H.lib().rdn_dense3_kernel_name(C.byref(d3), buf, 128), "rdn_dense3_kernel_name")
+        return buf.value.decode()
+
     def _dw_key(self, d, wg):
         dc = self._probe_copy(d, H.ConvDesc, _CONV_SELECT)
         wc = self._probe_copy(wg, H.WgradDesc, ("a_gate", "a_gate_alpha", "part"))
@@ -1049,7 +1056,7 @@ class UNetEngine:
                 # conv's output and PReLU input written once: 32 + 3 x 32 channels)
                 Ls = [by_name[f"{blk}.conv_{k}"] for k in range(3)]
                 fused_min = es * self.P[0] * (Ls[0].cin + sum(2 * x.cout for x in Ls))
-                L.extra["info"]["dense3"] = ("fwd", f"{blk}.conv_0-2", "conv3_dense_kernel<bf16,32,16>",
+                L.extra["info"]["dense3"] = ("fwd", f"{blk}.conv_0-2", self._dense3_key(L.extra["dense3"]),
                                              sum(p[3] for p in parts), sum(p[4] for p in parts), fused_min)
 
     # ------------------------------------------------------------------
