@@ -84,9 +84,10 @@ def main():
 
     def save():
         runs = [done[s] for s in seeds if s in done]
-        with open(args.out, "w") as f:
+        with open(args.out + ".tmp", "w") as f:   # (atomic: the run may be stopped at any time)
             json.dump({"config": CFG, "seed0": SEED0, "seed_stride": SEED_STRIDE, "threads_per_seed": 1,
                        "generator": "tests/golden/make_psnr_oracle.py", "runs": runs}, f, indent=0)
+        os.replace(args.out + ".tmp", args.out)
 
     with cf.ProcessPoolExecutor(args.workers, mp_context=mp.get_context("spawn")) as ex:
         futs = {ex.submit(one_seed, s): s for s in todo}

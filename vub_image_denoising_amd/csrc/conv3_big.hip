@@ -554,13 +554,25 @@ int launch_big(const rdn_conv_desc* d, hipStream_t st) {
 //   64 x 32 wave tiles, LDS-read heavier) with >= 8 chunk iterations per CU on
 //   >= 128 x 128 images, where the cross-item prefetch carries them (the level-1
 //   input gradients: 20-35 % faster than conv3_halo, up_0's 1.6x);
-// * 32-channel chunks only for single-chunk input gradients (a 5-chunk 160-channel
-//   forward measured slower than conv3_halo).
+// * 32-channel chunks: single-chunk input gradients and (round 4, with the k-step
+//   prefetch) the 5-chunk 160-channel level-1 conv_3 forward (big_ck32_multi).
+// multi-chunk 32-channel items: the 160-channel level-1 conv_3 forward (5 chunks; it
+// lost to conv3_halo in round 3, before the k-step prefetch; round 4, interleaved:
+// 82 -> 74 us per launch, step +0.5 % B16 / +0.4 % B32, profiles/r04_v13_big_ck32_ab.txt).
+// RDN_BIG_CK32=0: single-chunk 32-channel items only (A/B)
+bool big_ck32_multi() {
+  static const bool on = [] {
+    const char* e = getenv("RDN_BIG_CK32");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 template <int CK>
 int big_dispatch(const rdn_conv_desc* d, hipStream_t st) {
   const int64_t tiles = (int64_t)d->n * ((d->h + 15) / 16) * ((d->w + 15) / 16);
   const int cus = cu_count(), nch = d->cin / CK;
-  if (CK == 32 && nch != 1) return 1;
+  if (CK == 32 && nch != 1 && !big_ck32_multi()) return 1;
   auto even = [&](int64_t items) {
     const int64_t rounds = (items + cus - 1) / cus;
     return items >= cus && items * 10 >= rounds * cus * 9;
