@@ -580,13 +580,23 @@ int big_dispatch(const rdn_conv_desc* d, hipStream_t st) {
   // single-chunk and narrow-column launches won on the >= 128 x 128 images (level 1,
   // up_0) and lost on level 2's 64 x 64 ones (r03 per-layer A/B)
   const bool big_img = (int64_t)d->h * d->w >= 128 * 128;
+  // Round 4 (with the k-step prefetch), per-layer A/B on the train step at B16 / B32
+  // (profiles/r04_v14_big_loose_layers.txt): the 128-column items now win on any evenly
+  // spread grid (level-2 conv_2 input gradient 55 -> 48 / 104 -> 88 us, conv_0 -3 / -5
+  // us) and so do the 64-column ones (level-2 conv_0..2 forward -1..-2 / -6..-13 us);
+  // the 96-column (conv_1 dgrad: even) and 80-column ones (conv_3 dgrad: +4 / +16 us)
+  // keep the round-3 rule.  RDN_BIG_LOOSE=0: the round-3 rule everywhere.
+  static const bool loose = [] {
+    const char* e = getenv("RDN_BIG_LOOSE");
+    return !(e && e[0] == '0');
+  }();
   auto wide_ok = [&](int bn) {
     const int64_t items = tiles * (d->ncols / bn);
-    return even(items) && (nch >= 2 || (items >= 4ll * cus && big_img));
+    return even(items) && ((loose && bn == 128) || nch >= 2 || (items >= 4ll * cus && big_img));
   };
   auto narrow_ok = [&](int bn) {
     const int64_t items = tiles * (d->ncols / bn);
-    return even(items) && items * nch >= 8ll * cus && big_img;
+    return even(items) && ((loose && bn == 64) || (items * nch >= 8ll * cus && big_img));
   };
   if (d->ncols % 128 == 0) return wide_ok(128) ? launch_big<16, 128, 4, CK>(d, st) : 1;
   if (d->ncols % 96 == 0) return wide_ok(96) ? launch_big<16, 96, 4, CK>(d, st) : 1;
