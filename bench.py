@@ -603,6 +603,8 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         if args.dist_backend == "nccl":
+            from vub_image_denoising_amd.ddp import capture_safe_env
+            capture_safe_env()   # (RCCL inside the captured train step)
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")

@@ -107,6 +107,8 @@ def _rccl_worker(init_file, q):
         import torch.distributed as dist
         torch.cuda.set_device(0)
         dev = torch.device("cuda", 0)
+        from vub_image_denoising_amd.ddp import capture_safe_env
+        capture_safe_env()
         dist.init_process_group("nccl", init_method=f"file://{init_file}", rank=0, world_size=1, device_id=dev)
         import vub_image_denoising_amd as vm
         from vub_image_denoising_amd.ddp import GradSync

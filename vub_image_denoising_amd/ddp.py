@@ -31,8 +31,21 @@ wrapper around DiffusionModel anyway.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
+
+
+def capture_safe_env() -> None:
+    """Environment for RCCL collectives inside a captured hipGraph; call before
+    ``init_process_group``.  ProcessGroupNCCL's watchdog polls the end events of
+    eager collectives (the warm-up steps before capture); with its event cache on, a
+    cached event can be recorded again inside the capture while an older work item
+    still holds it, and the watchdog's query then fails with hipErrorCapturedEvent
+    and aborts the process (seen once in the world-1 graph test on MI355X, round 4).
+    Without the cache every work item owns its events."""
+    os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
 
 
 def plan_buckets(sizes, offsets, bucket_elems):
