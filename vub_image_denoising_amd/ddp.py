@@ -39,12 +39,9 @@ import torch.distributed as dist
 
 def capture_safe_env() -> None:
     """Environment for RCCL collectives inside a captured hipGraph; call before
-    ``init_process_group``.  ProcessGroupNCCL's watchdog polls the end events of
-    eager collectives (the warm-up steps before capture); with its event cache on, a
-    cached event can be recorded again inside the capture while an older work item
-    still holds it, and the watchdog's query then fails with hipErrorCapturedEvent
-    and aborts the process (seen once in the world-1 graph test on MI355X, round 4).
-    Without the cache every work item owns its events."""
+    ``init_process_group``: no NCCL event cache (every work item owns its events, so
+    no event of an eager collective is re-recorded inside a capture).  The capture
+    itself first drains the watchdog's pending works (train_graph._drain_collectives)."""
     os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
 
 

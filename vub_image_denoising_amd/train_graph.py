@@ -33,6 +33,27 @@ from .engine import find_flat
 from .optim import FusedAdam
 
 
+def _drain_collectives(fp) -> None:
+    """Before a capture: wait until ProcessGroupNCCL's watchdog has retired every
+    eager collective (the warm-up steps' all-reduces).  Its loop queries each
+    pending work's end event, recorded on the group's RCCL stream; once that stream
+    is pulled into the capture, HIP refuses the query (hipErrorCapturedEvent) and the
+    watchdog aborts the process -- seen in the world-1 graph test on MI355X, round 4,
+    whenever the capture began before the watchdog's next sweep."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return
+    sync = getattr(fp, "grad_sync", None) if fp is not None else None
+    groups = [dist.group.WORLD] + ([sync.group] if sync is not None and sync.group is not None else [])
+    for pg in groups:
+        try:
+            if dist.get_backend(pg) != "nccl":
+                continue
+        except (RuntimeError, ValueError):
+            continue
+        pg._wait_for_pending_works()
+
+
 def _node_count(g):
     """Kernel/memset/copy nodes of a captured graph (None if not exposed)."""
     try:
@@ -104,6 +125,7 @@ class TrainStepGraph:
             opt._step_dev.fill_(opt._step)
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize(self.dev)
+        _drain_collectives(fp)
         fp.generation += 1
         for wp in self.model.unet._rdn_packs.values():
             wp.key = None          # the weight repack is the graph's first launch
