@@ -568,6 +568,14 @@ bool big_ck32_multi() {
   return on;
 }
 
+bool big_fall() {
+  static const bool on = [] {
+    const char* e = getenv("RDN_BIG_FALL");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 template <int CK>
 int big_dispatch(const rdn_conv_desc* d, hipStream_t st) {
   const int64_t tiles = (int64_t)d->n * ((d->h + 15) / 16) * ((d->w + 15) / 16);
@@ -600,7 +608,14 @@ int big_dispatch(const rdn_conv_desc* d, hipStream_t st) {
   };
   if (d->ncols % 128 == 0) return wide_ok(128) ? launch_big<16, 128, 4, CK>(d, st) : 1;
   if (d->ncols % 96 == 0) return wide_ok(96) ? launch_big<16, 96, 4, CK>(d, st) : 1;
-  if (d->ncols % 80 == 0) return narrow_ok(80) ? launch_big<16, 80, 8, CK>(d, st) : 1;
+  if (d->ncols % 80 == 0) {
+    if (narrow_ok(80)) return launch_big<16, 80, 8, CK>(d, st);
+    // the 320-column level-2 conv_3 input gradient on 64-column items (<= 6 per CU):
+    // faster alone (B16 72-77 -> 67-69 us, profiles/r04_v17_big_fall_layers.txt) but
+    // slower in the step beside the weight-gradient stream (1715 -> 1708 img/s,
+    // interleaved, r04_v18_big_fall_ab.txt): off, RDN_BIG_FALL=1 for A/B
+    if (!(big_fall() && d->ncols % 64 == 0 && tiles * (d->ncols / 64) <= 6ll * cus)) return 1;
+  }
   if (d->ncols % 64 == 0) return narrow_ok(64) ? launch_big<16, 64, 4, CK>(d, st) : 1;
   if (d->ncols == 32) {
     // the narrow level-1 forwards (64 / 128 input channels -> 32; 32 x 32 wave tiles,
