@@ -1,0 +1,44 @@
+"""dYpre / partial / slab slots of the weight-gradient stream (engine.py, round 4):
+one slot per layer while their buffers fit RDN_SLOT_BUDGET of the free device
+memory, else the 6-slot ring (the dgrad chain then waits for the side stream where
+it reuses a slot).  Scheduling only: the gradients are bit-identical either way, and
+the choice is made once per engine pool (its engines share the slot buffers)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _grads(budget, B=2, S=256, seed=0):
+    import vub_image_denoising_amd as vm
+    from vub_image_denoising_amd import engine as E
+    old = E.SLOT_BUDGET
+    E.SLOT_BUDGET = budget
+    try:
+        torch.manual_seed(seed)
+        m = vm.RDUNet_T(base_filters=32).cuda()
+        m.set_compute_dtype("bf16")
+        g = torch.Generator().manual_seed(seed + 1)
+        x = (torch.rand(B, 3, S, S, generator=g) * 2 - 1).cuda()
+        t = torch.rand(B, 1, 1, 1, generator=g).cuda()
+        w = torch.randn(B, 3, S, S, generator=g).cuda()
+        grads = []
+        for _ in range(2):   # two forwards, one backward each: the pool's second engine too
+            m.zero_grad(set_to_none=True)
+            y = m(x, t)
+            (y * w).mean().backward()
+            grads.append({n: p.grad.detach().clone() for n, p in m.named_parameters()})
+        slots = {eng.slots for pool in m._rdn_engines.values() for eng in pool if eng.train}
+        nlayers = {len(eng.layers) for pool in m._rdn_engines.values() for eng in pool if eng.train}
+        return grads, slots, nlayers
+    finally:
+        E.SLOT_BUDGET = old
+
+
+def test_slot_budget_ring_bit_identical():
+    g_all, s_all, n_all = _grads(1e9)
+    g_ring, s_ring, _ = _grads(0.0)
+    assert s_all == n_all and s_ring == {6}, (s_all, s_ring, n_all)
+    for a, b in zip(g_all, g_ring):
+        for n in a:
+            assert torch.equal(a[n], b[n]), n

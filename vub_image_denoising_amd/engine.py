@@ -193,7 +193,8 @@ WGRAD_STREAM = os.environ.get("RDN_WGRAD_STREAM", "1") != "0"
 # replayed graph -- 1739 / 1742 against 1723 / 1724 with 6, profiles/r03_v11_slots_ab.txt;
 # all interleaved on one box.  Memory: the dYpre / partial / slab buffers of every layer,
 # ~1.5 GB at B16)
-WGRAD_SLOTS = int(os.environ.get("RDN_WGRAD_SLOTS", "0"))   # 0: one slot per layer
+WGRAD_SLOTS = int(os.environ.get("RDN_WGRAD_SLOTS", "0"))   # 0: one slot per layer (within SLOT_BUDGET)
+SLOT_BUDGET = float(os.environ.get("RDN_SLOT_BUDGET", "0.25"))   # fraction of free device memory
 # With one slot per layer the captured graph has no edge from the weight-gradient branch
 # back into the dgrad chain, and the replay enqueues the whole chain before the branch:
 # harmless while the host enqueues a replay in ~1 ms, but under a profiler (slower
@@ -624,8 +625,18 @@ class UNetEngine:
             self.side = torch.cuda.Stream(device=dev) if (dev.type == "cuda" and WGRAD_STREAM) else None
             if self.side is None:
                 self.slots = 1
+            elif WGRAD_SLOTS > 0:
+                self.slots = min(WGRAD_SLOTS, len(layers))
             else:
-                self.slots = len(layers) if WGRAD_SLOTS <= 0 else min(WGRAD_SLOTS, len(layers))
+                # one slot per layer while its dYpre buffers stay within a quarter of the
+                # free device memory (1.5 GB at B16 256^2, 6 GB at B64 or 512^2 crops;
+                # RDN_SLOT_BUDGET), else the 6-slot ring of round 3 (-1 % step)
+                # (decided once per pool: its engines share the slot buffers)
+                def pick():
+                    need = sum(self.P[self._out_level(L)] * L.cout_pad for L in layers) * (2 if dtype == torch.bfloat16 else 4)
+                    free = torch.cuda.mem_get_info(dev)[0]
+                    return len(layers) if need <= SLOT_BUDGET * free else min(6, len(layers))
+                self.slots = self._shared("slots", pick)
             sizes = [0] * self.slots
             for b, L in enumerate(reversed(layers)):
                 sizes[b % self.slots] = max(sizes[b % self.slots], self.P[self._out_level(L)] * L.cout_pad)
