@@ -170,6 +170,18 @@ int rdn_wgrad_reduce(const float* ws, int32_t splits, int32_t mdim, int32_t ndim
 int rdn_wgrad_reduce_cols(const float* ws, int32_t splits, int32_t mdim, int32_t ndim, int32_t taps, float* grad,
                           int32_t grad_ci_total, int32_t grad_ci0, int32_t accumulate, const float* part,
                           int32_t part_splits, float* dalpha, float* dbias, void* stream);
+/* Up to RDN_REDUCE_BATCH_MAX of these reductions in ONE launch (round 4: the fused
+   layers' reduces on the compute stream are latency-bound, one launch each).  A job
+   is rdn_wgrad_reduce_cols's arguments (ndim_real <= ndim: rdn_wgrad_reduce's
+   ndim_real with gstride = ndim_real, gci0 = 0); sl / blocks / pblocks are filled in
+   by the call.  Results bit-identical to the single launches. */
+#define RDN_REDUCE_BATCH_MAX 8
+typedef struct rdn_reduce_job {
+  const float* ws; float* grad; const float* part; float* dalpha; float* dbias;
+  int32_t splits, mdim, ndim, ndim_real, taps, gstride, gci0, accumulate, part_splits;
+  int32_t sl, blocks, pblocks;   /* (set by rdn_wgrad_reduce_batch) */
+} rdn_reduce_job;
+int rdn_wgrad_reduce_batch(const rdn_reduce_job* jobs, int32_t n, void* stream);
 
 /* Fused input gradient + weight gradient of one gated 3x3 conv (the narrow level-0
    layers: dgrad->cin = 16|32 dY channels, dgrad->ncols = wgrad->ndim = 32..80 input

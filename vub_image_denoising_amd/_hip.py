@@ -65,6 +65,16 @@ class Dense3Desc(C.Structure):
     ]
 
 
+class ReduceJob(C.Structure):
+    _fields_ = [("ws", _vp), ("grad", _vp), ("part", _vp), ("dalpha", _vp), ("dbias", _vp),
+                ("splits", _i32), ("mdim", _i32), ("ndim", _i32), ("ndim_real", _i32), ("taps", _i32),
+                ("gstride", _i32), ("gci0", _i32), ("accumulate", _i32), ("part_splits", _i32),
+                ("sl", _i32), ("blocks", _i32), ("pblocks", _i32)]
+
+
+REDUCE_BATCH_MAX = 8
+
+
 class PackItem(C.Structure):
     _fields_ = [("w", _vp), ("out", _vp), ("mode", _i32), ("d0", _i32), ("d1", _i32), ("kh", _i32), ("kw", _i32),
                 ("pad0", _i32), ("pad1", _i32), ("rows_pad", _i32), ("kp", _i32), ("ck", _i32)]
@@ -94,6 +104,7 @@ SIGNATURES = {
     "rdn_wgrad_workspace_size": (_i64, [C.POINTER(WgradDesc)]),
     "rdn_wgrad_reduce": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _vp, _i32, _vp, _i32, _vp, _vp, _vp]),
     "rdn_wgrad_reduce_cols": (_i32, [_vp, _i32, _i32, _i32, _i32, _vp, _i32, _i32, _i32, _vp, _i32, _vp, _vp, _vp]),
+    "rdn_wgrad_reduce_batch": (_i32, [C.POINTER(ReduceJob), _i32, _vp]),
     "rdn_prelu_bwd_blocks": (_i32, [_i32, _i64, _i32]),
     "rdn_prelu_bwd": (_i32, [_i32, _i64, _i32, _i32, _i32, _i32, _i32, _vp, _i64, _i32, _i64, _vp, _vp, _i64, _vp,
                              _vp, _vp, _vp, _vp, _vp]),

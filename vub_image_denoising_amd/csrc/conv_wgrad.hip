@@ -189,14 +189,16 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(rdn_wgrad_desc d, FastDiv fd_
 // thread sums splits sl, sl+SL, ... and the SL partials are added in a fixed
 // order through LDS (deterministic).  The result goes to the reference layout
 // [m][nd][tap] (OIHW / IOHW).
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int mdim, int ndim,
-                                                           int ndim_real, int taps, float* __restrict__ grad,
-                                                           int accumulate, int sl_count, const float* __restrict__ part,
-                                                           int part_splits, float* __restrict__ dalpha,
-                                                           float* __restrict__ dbias, int gstride, int gci0) {
-  if (blockIdx.y == 1) {  // fused-PReLU partials: one block per (channel, dalpha|dbias), fixed order
-    if (blockIdx.x >= 2 * mdim) return;
-    const int which = blockIdx.x / mdim, m = blockIdx.x - which * mdim;
+// one block of a reduction: slab block `bx` (part == false) or partial block `bx`
+// (part == true: one per (channel, dalpha|dbias), fixed order)
+__device__ __forceinline__ void wgrad_reduce_block(const float* __restrict__ ws, int splits, int mdim, int ndim,
+                                                   int ndim_real, int taps, float* __restrict__ grad, int accumulate,
+                                                   int sl_count, const float* __restrict__ part, int part_splits,
+                                                   float* __restrict__ dalpha, float* __restrict__ dbias, int gstride,
+                                                   int gci0, int bx, bool is_part) {
+  if (is_part) {  // fused-PReLU partials
+    if (bx >= 2 * mdim) return;
+    const int which = bx / mdim, m = bx - which * mdim;
     float s = 0.f;
     for (int z = threadIdx.x; z < part_splits; z += 256) s += part[((int64_t)z * 2 + which) * mdim + m];
     __shared__ float red1[256];
@@ -218,7 +220,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   const int cq = threadIdx.x % qpb, sl = threadIdx.x / qpb;
   const int ncol = taps * ndim;
   const int64_t total = (int64_t)mdim * ncol;     // multiple of 4 (ndim % 8 == 0)
-  const int64_t o = ((int64_t)blockIdx.x * qpb + cq) * 4;
+  const int64_t o = ((int64_t)bx * qpb + cq) * 4;
   f32x4 s = {0.f, 0.f, 0.f, 0.f};
   if (o < total) {
     const float* p = ws + o;
@@ -249,6 +251,37 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
       }
     }
   }
+}
+
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int mdim, int ndim,
+                                                           int ndim_real, int taps, float* __restrict__ grad,
+                                                           int accumulate, int sl_count, const float* __restrict__ part,
+                                                           int part_splits, float* __restrict__ dalpha,
+                                                           float* __restrict__ dbias, int gstride, int gci0) {
+  wgrad_reduce_block(ws, splits, mdim, ndim, ndim_real, taps, grad, accumulate, sl_count, part, part_splits, dalpha,
+                     dbias, gstride, gci0, blockIdx.x, blockIdx.y == 1);
+}
+
+// Several reductions in ONE launch (round 4): the fused dgrad+wgrad layers' reduces
+// run on the compute stream, one small latency-bound launch per layer (40 per B16
+// step, ~7 us each against ~2-3 us of slab bytes); consecutive ones go together.
+// Job j owns blocks [beg[j], beg[j+1]): its slab blocks, then its partial blocks.
+// Same per-block work and summation order as the single launches (bit-identical).
+struct ReduceBatch {
+  rdn_reduce_job job[RDN_REDUCE_BATCH_MAX];
+  int32_t beg[RDN_REDUCE_BATCH_MAX + 1];
+  int32_t n;
+};
+
+__global__ __launch_bounds__(256) void wgrad_reduce_batch_kernel(ReduceBatch b) {
+  int j = 0;
+  while (j + 1 < b.n && (int)blockIdx.x >= b.beg[j + 1]) ++j;
+  const rdn_reduce_job& q = b.job[j];
+  const int bx = (int)blockIdx.x - b.beg[j];
+  const bool is_part = bx >= q.blocks;
+  wgrad_reduce_block(q.ws, q.splits, q.mdim, q.ndim, q.ndim_real, q.taps, q.grad, q.accumulate, q.sl, q.part,
+                     q.part_splits > 0 ? q.part_splits : q.splits, q.dalpha, q.dbias, q.gstride, q.gci0,
+                     is_part ? bx - q.blocks : bx, is_part);
 }
 
 struct Cfg { int bm, bn; };
@@ -342,6 +375,17 @@ extern "C" int rdn_conv_wgrad(const rdn_wgrad_desc* d, void* stream) {
   return d->dtype == RDN_BF16 ? launch_t<bf16>(d, st) : launch_t<float>(d, st);
 }
 
+// split lanes per column quad: only as many as it takes to give the launch ~64k
+// threads (one per lane of every SIMD); each lane then streams its splits with
+// four loads in flight.  (Lanes for every split up to 16 -- the previous rule --
+// left the wide level-2/3 reductions at one or two loads per thread: 0.7 TB/s.)
+static int reduce_lanes(int64_t total, int splits) {
+  const int64_t quads = total / 4;
+  int sl = 1;
+  while (sl < 16 && sl < splits && quads * sl < 65536) sl <<= 1;
+  return sl;
+}
+
 static int wgrad_reduce_impl(const float* ws, int32_t splits, int32_t mdim, int32_t ndim, int32_t ndim_real,
                              int32_t taps, float* grad, int32_t gstride, int32_t gci0, int32_t accumulate,
                              const float* part, int32_t part_splits, float* dalpha, float* dbias, void* stream) {
@@ -351,13 +395,7 @@ static int wgrad_reduce_impl(const float* ws, int32_t splits, int32_t mdim, int3
   }
   const int64_t total = (int64_t)mdim * ndim * taps;
   if (ndim % 4 || ((uintptr_t)ws & 15)) { rdn_set_error("rdn_wgrad_reduce: ndim %% 4 / alignment"); return RDN_E_ARG; }
-  // split lanes per column quad: only as many as it takes to give the launch ~64k
-  // threads (one per lane of every SIMD); each lane then streams its splits with
-  // four loads in flight.  (Lanes for every split up to 16 -- the previous rule --
-  // left the wide level-2/3 reductions at one or two loads per thread: 0.7 TB/s.)
-  const int64_t quads = total / 4;
-  int sl = 1;
-  while (sl < 16 && sl < splits && quads * sl < 65536) sl <<= 1;
+  const int sl = reduce_lanes(total, splits);
   const int qpb = 256 / sl;
   int64_t blocks = (total / 4 + qpb - 1) / qpb;
   if (part && blocks < 2 * mdim) blocks = 2 * mdim;
@@ -382,4 +420,34 @@ extern "C" int rdn_wgrad_reduce_cols(const float* ws, int32_t splits, int32_t md
                                      void* stream) {
   return wgrad_reduce_impl(ws, splits, mdim, ndim, ndim, taps, grad, grad_ci_total, grad_ci0, accumulate, part,
                            part_splits, dalpha, dbias, stream);
+}
+
+// Up to RDN_REDUCE_BATCH_MAX reductions (each as rdn_wgrad_reduce_cols would run it:
+// ws, splits, mdim, ndim, ndim_real, taps, grad + gstride / gci0, accumulate, the
+// fused-PReLU partials) in one launch; sl / blocks are filled in here.
+extern "C" int rdn_wgrad_reduce_batch(const rdn_reduce_job* jobs, int32_t n, void* stream) {
+  if (!jobs || n <= 0 || n > RDN_REDUCE_BATCH_MAX) { rdn_set_error("rdn_wgrad_reduce_batch: 1..%d jobs", RDN_REDUCE_BATCH_MAX); return RDN_E_ARG; }
+  ReduceBatch b{};
+  b.n = n;
+  int64_t acc = 0;
+  for (int j = 0; j < n; ++j) {
+    rdn_reduce_job q = jobs[j];
+    if (!q.ws || !q.grad || q.splits <= 0 || q.mdim <= 0 || q.ndim <= 0 || q.ndim_real <= 0 || q.ndim_real > q.ndim ||
+        q.taps <= 0 || q.gci0 < 0 || q.gci0 + q.ndim_real > q.gstride || q.ndim % 4 || ((uintptr_t)q.ws & 15)) {
+      rdn_set_error("rdn_wgrad_reduce_batch: job %d: bad arguments", j);
+      return RDN_E_ARG;
+    }
+    const int64_t total = (int64_t)q.mdim * q.ndim * q.taps;
+    q.sl = reduce_lanes(total, q.splits);
+    const int qpb = 256 / q.sl;
+    q.blocks = (int32_t)((total / 4 + qpb - 1) / qpb);
+    q.pblocks = q.part ? 2 * q.mdim : 0;
+    b.job[j] = q;
+    b.beg[j] = (int32_t)acc;
+    acc += (int64_t)q.blocks + q.pblocks;
+  }
+  if (acc > 0x7fffffff) { rdn_set_error("rdn_wgrad_reduce_batch: too large"); return RDN_E_SHAPE; }
+  b.beg[n] = (int32_t)acc;
+  wgrad_reduce_batch_kernel<<<(unsigned)acc, 256, 0, (hipStream_t)stream>>>(b);
+  return rdn_check_launch("rdn_wgrad_reduce_batch");
 }

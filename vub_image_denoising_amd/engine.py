@@ -226,6 +226,9 @@ GATE_OUT = os.environ.get("RDN_GATE_OUT", "1") == "1"
 # gate-out in the fused dgrad+wgrad kernel (conv3_dw ",go": up_0.conv finishing
 # up_0.conv_t, the level-1 conv_0s finishing down_0 / the previous block's conv_3)
 GATE_OUT_DW = os.environ.get("RDN_GATE_OUT_DW", "1") == "1"
+# the fused layers' split-K reduces of consecutive fused layers in one launch
+# (rdn_wgrad_reduce_batch; RDN_REDUCE_BATCH=0: one launch per layer)
+REDUCE_BATCH = os.environ.get("RDN_REDUCE_BATCH", "1") != "0"
 # conv_0..conv_2 of every level-0 DenoisingBlock (base_filters 32, bf16) as ONE
 # launch that reads x once and keeps out_0 / out_1 on chip (rdn_dense3_fwd)
 FUSE_DENSE = os.environ.get("RDN_DENSE", "1") != "0"
@@ -1154,7 +1157,33 @@ class UNetEngine:
             sst = st
         tr = TRACER
         rev = list(reversed(self.layers))
+        pending = []   # fused layers whose split-K reduces wait for one batched launch
+
+        def flush():
+            if not pending:
+                return
+            jl = [j for _, js in pending for j in js]
+            for i in range(0, len(jl), H.REDUCE_BATCH_MAX):
+                n_ = min(H.REDUCE_BATCH_MAX, len(jl) - i)
+                H.check(lib.rdn_wgrad_reduce_batch((H.ReduceJob * n_)(*jl[i:i + n_]), n_, st), "wgrad_reduce_batch")
+            for Lp, _ in pending:
+                if side is not None:
+                    Lp.extra["ev_done"].record(main)
+                if sync is not None:
+                    sync.params_done(Lp.extra["pidx"], stream=None if side is None else main)
+            pending.clear()
+
+        def wait_done(Lw):
+            """The compute stream waits for layer Lw's weight-gradient work (its slot
+            free / an ordering edge); a still-batched fused layer is flushed first, so
+            its event is recorded in this pass before the wait."""
+            if any(Lp is Lw for Lp, _ in pending):
+                flush()
+            main.wait_event(Lw.extra["ev_done"])
+
         for b, L in enumerate(rev):
+            if pending and not L.extra["dw"]:
+                flush()
             info = L.extra["info"]
             olvl = L.extra["olvl"]
             n, h, w = self.grid[olvl]
@@ -1163,7 +1192,7 @@ class UNetEngine:
             fused = L.extra["fused"]
             if side is not None and ORDER_EVERY and b >= ORDER_EVERY and b % ORDER_EVERY == 0 and b < self.slots:
                 # ordering edge only (no buffer is reused): see ORDER_EVERY
-                main.wait_event(rev[b - ORDER_EVERY].extra["ev_done"])
+                wait_done(rev[b - ORDER_EVERY])
             dyp, pws = L.extra["dyp"], L.extra["pws"]
             # unfused: the PReLU-backward pass leaves its dalpha/dbias partials in
             # pws for this layer's rdn_wgrad_reduce to sum (no finalize launch);
@@ -1172,7 +1201,7 @@ class UNetEngine:
                 rc = 0
             else:
                 if side is not None and b >= self.slots:
-                    main.wait_event(rev[b - self.slots].extra["ev_done"])
+                    wait_done(rev[b - self.slots])
                 if L.ddst is None:
                     tok = tr.start(info["prelu"]) if tr is not None else None
                     rc = lib.rdn_prelu_bwd(self.code, P, n, h, w, L.cout, L.cout_pad, None, 0, 0, 0, dy.data_ptr(),
@@ -1194,11 +1223,11 @@ class UNetEngine:
                 # partials go to this ring slot's buffers, free once the side stream
                 # reduced the layer that used the slot before
                 if side is not None and b >= self.slots:
-                    main.wait_event(rev[b - self.slots].extra["ev_done"])
+                    wait_done(rev[b - self.slots])
                 K = L.extra.get("gates")
                 if K is not None and side is not None and K.extra["bidx"] >= self.slots:
                     # (gate-out) this epilogue writes K's dYpre / partials into K's ring slot
-                    main.wait_event(rev[K.extra["bidx"] - self.slots].extra["ev_done"])
+                    wait_done(rev[K.extra["bidx"] - self.slots])
                 tok = tr.start(info["dw"]) if tr is not None else None
                 rc = lib.rdn_conv_dgrad_wgrad(C.byref(L.dgrad_desc), C.byref(L.wgrad_desc), st)
                 if tok is not None:
@@ -1213,7 +1242,7 @@ class UNetEngine:
                 K = L.extra.get("gates")
                 if K is not None and side is not None and K.extra["bidx"] >= self.slots:
                     # this epilogue writes K's dYpre / partials into K's ring slot
-                    main.wait_event(rev[K.extra["bidx"] - self.slots].extra["ev_done"])
+                    wait_done(rev[K.extra["bidx"] - self.slots])
                 if L.src.buf not in self.pure_inputs or need_buf[L.src.buf]:
                     tok = tr.start(info["dgrad"]) if tr is not None else None
                     rc = lib.rdn_conv_fwd(C.byref(L.dgrad_desc), st)
@@ -1241,6 +1270,21 @@ class UNetEngine:
                            else lib.rdn_prelu_bwd_blocks(self.code, P, L.cout_pad))
             ow, ob, oa = L.extra["goff"]
             cols = L.extra["dw_cols"]
+            if dw and REDUCE_BATCH:
+                # (a fused layer's reduce joins the batch of consecutive fused layers,
+                # one launch on the compute stream: flushed before the next unfused layer)
+                jobs = []
+                nh = ndim // cols
+                sh = splits // nh
+                for hh in range(nh):
+                    jobs.append(H.ReduceJob(
+                        ws=L.wgrad_desc.ws + hh * sh * mdim * taps * cols * 4, grad=gbase + ow,
+                        part=pws if hh == 0 else None, dalpha=gbase + oa, dbias=gbase + ob,
+                        splits=sh, mdim=mdim, ndim=cols if nh > 1 else ndim, ndim_real=cols if nh > 1 else ndim_real,
+                        taps=taps, gstride=ndim_real, gci0=hh * cols, accumulate=1,
+                        part_splits=sh if nh > 1 else part_splits))
+                pending.append((L, jobs))
+                continue
             if cols < ndim:
                 # column halves of the fused kernel: each half's slabs hold its input
                 # channels; the dalpha/dbias partials are half 0's rows
@@ -1260,6 +1304,7 @@ class UNetEngine:
                 L.extra["ev_done"].record(main if rst == st else side)
             if sync is not None:   # the stream this layer's gradients were completed on
                 sync.params_done(L.extra["pidx"], stream=None if side is None else (main if rst == st else side))
+        flush()
         if side is not None:
             self.ev_end.record(side)
             main.wait_event(self.ev_end)
