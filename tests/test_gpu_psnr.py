@@ -22,7 +22,7 @@ The GPU legs train here, in fp32 and bf16, as one captured train step per dtype
 The statistic is the per-seed difference GPU - oracle: its mean and two-sided 95 %
 Student-t interval.  Training is chaotic (fp32 rounding differences of a few ulps
 grow over 120 steps: sd ~0.17 dB per seed, profiles/r02_psnr_sigma25_paired.json),
-so >= 130 seeds are needed for a half-width <= 0.03 dB; the test runs 288 (~0.02 dB:
+so >= 130 seeds are needed for a half-width <= 0.03 dB; the test runs 216 (~0.022 dB:
 at 144 a correct build still failed the +-0.05 dB CI bound about one time in eight,
 since any mean beyond +-0.022 dB did).  Asserted: the oracle leg gains
 >= 3 dB over the noisy input at 64x64 and beats the noisy input at 256x256; both
@@ -53,7 +53,8 @@ from oracle.weights import make_params  # noqa: E402
 
 FIXTURE = os.path.join(REPO, "tests", "golden", "psnr_sigma25_oracle.json")
 MIN_SEEDS = 130   # half-width <= 0.03 dB at sd ~0.17 dB
-MAX_SEEDS = 288   # the first 288 of the fixture (half-width ~0.02 dB; ~1.5 s of GPU test per seed)
+MAX_SEEDS = 216   # the first 216 of the fixture (half-width ~0.022 dB; ~1 s of GPU test per seed,
+#                   so the whole -m gpu suite stays near 7 minutes)
 
 
 def _stats(d):
