@@ -45,6 +45,21 @@ def test_plan_buckets_cover_everything_once():
     assert any(hi - lo >= 900000 for lo, hi in covered)
 
 
+def test_plan_buckets_small_tail():
+    """The start of the flat buffer (completes last) gets a small bucket of its own."""
+    fp = _fake_flat(0, SIZES)
+    b0 = plan_buckets(SIZES, fp.offsets, 1000000)
+    b = plan_buckets(SIZES, fp.offsets, 1000000, tail_elems=80000)
+    assert len(b) == len(b0) + 1
+    hi_prev = None
+    for lo, hi, first in b:
+        hi = fp.numel if hi is None else hi
+        assert hi_prev is None or hi == hi_prev
+        assert lo == fp.offsets[first]
+        hi_prev = lo
+    assert b[-1][0] == 0 and 0 < b[-1][1] <= 80000 and b[-1][1] in fp.offsets
+
+
 def _worker(rank, world, init_file, q, defer=False):
     # file:// rendezvous: no TCP port to race for between parallel test runs
     dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)

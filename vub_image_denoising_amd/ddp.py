@@ -45,10 +45,17 @@ def capture_safe_env() -> None:
     os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
 
 
-def plan_buckets(sizes, offsets, bucket_elems):
+def plan_buckets(sizes, offsets, bucket_elems, tail_elems=0):
     """Group parameters (given in flat order) into contiguous buckets, filling
     from the END of the flat buffer (first gradients to complete).  Returns a
-    list of (lo, hi, first_param_index) with flat ranges [lo, hi)."""
+    list of (lo, hi, first_param_index) with flat ranges [lo, hi).
+
+    ``tail_elems``: the bucket at the START of the buffer (input block and encoder
+    level 0/1: the gradients that complete last) is its all-reduce that nothing
+    overlaps; it is cut down to the parameters within the first ``tail_elems``
+    elements, the rest of it becoming a bucket of its own that is launched as soon
+    as the encoder's deeper levels are done (39.7 MB at base_filters 32, 25-MB buckets:
+    21.3 + 18.4 MB -> 21.3 + 15.3 + 3.1 MB, the exposed tail 6x smaller)."""
     n = len(sizes)
     buckets = []
     hi_idx = n
@@ -62,19 +69,30 @@ def plan_buckets(sizes, offsets, bucket_elems):
         hi = offsets[hi_idx] if hi_idx < n else None
         buckets.append((lo, hi, lo_idx))
         hi_idx = lo_idx
+    if tail_elems > 0 and buckets:
+        lo, hi, first = buckets[-1]
+        end = hi if hi is not None else (offsets[-1] + sizes[-1])
+        if end - lo <= tail_elems:
+            return buckets
+        k = 0
+        while k + 1 < n and offsets[k + 1] <= tail_elems and (hi is None or offsets[k + 1] < hi):
+            k += 1
+        if 0 < k and offsets[k] < end:
+            buckets[-1] = (offsets[k], hi, k)
+            buckets.append((0, offsets[k], 0))
     return buckets
 
 
 class GradSync:
     """Bucketed, backward-overlapped gradient all-reduce for a FlatParams."""
 
-    def __init__(self, fp, bucket_mb: float = 25.0, group=None, overlap: bool = True):
+    def __init__(self, fp, bucket_mb: float = 25.0, group=None, overlap: bool = True, tail_mb: float = 4.0):
         self.fp = fp
         self.group = group
         self.world = dist.get_world_size(group)
         sizes = [p.numel() for p in fp.params]
         offs = list(fp.offsets)
-        raw = plan_buckets(sizes, offs, int(bucket_mb * 2 ** 20 / 4))
+        raw = plan_buckets(sizes, offs, int(bucket_mb * 2 ** 20 / 4), int(tail_mb * 2 ** 20 / 4))
         self.buckets = []
         self.param_bucket = [0] * len(sizes)
         hi_idx = len(sizes)
