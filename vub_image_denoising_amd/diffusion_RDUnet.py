@@ -123,9 +123,9 @@ def train_step_device(model, clean_images, noisy_images, optimizer, distribution
             sync._average()   # gradients not the flat views: average them first
             pre = None
         if pre is not None:
-            Fn.clip_grad_norm_flat(flat, clip_value, pre_scale=pre)                    # :113
+            Fn.clip_grad_norm_flat(flat, clip_value, pre_scale=pre, want_norm=False)   # :113
         else:
-            Fn.clip_grad_norm_(params, clip_value)                                     # :113
+            Fn.clip_grad_norm_(params, clip_value, want_norm=False)                    # :113
     return loss
 
 

@@ -107,12 +107,14 @@ def combined_loss(pred, target, mse_weight=0, charbonnier_weight=1, ssim_weight=
     return loss
 
 
-def clip_grad_norm_flat(fp: FlatParams, max_norm: float, pre_scale: float = 1.0) -> torch.Tensor:
+def clip_grad_norm_flat(fp: FlatParams, max_norm: float, pre_scale: float = 1.0, want_norm: bool = True):
     """Global L2 norm of the flat gradient and in-place scale by
     min(max_norm/(norm+1e-6), 1) — torch.nn.utils.clip_grad_norm_ semantics,
     without a host synchronisation.  Returns the (device) total norm.
     ``pre_scale``: a factor not yet applied to the gradient (the data-parallel
-    1/world average, ddp.GradSync.defer_average), folded into the same scale pass."""
+    1/world average, ddp.GradSync.defer_average), folded into the same scale pass.
+    ``want_norm=False`` (the train step, which discards it): no copy of the norm out of
+    the workspace (one launch less in the captured step); returns None."""
     lib = H.lib()
     ws = getattr(fp, "_clip_ws", None)
     if ws is None:
@@ -123,10 +125,10 @@ def clip_grad_norm_flat(fp: FlatParams, max_norm: float, pre_scale: float = 1.0)
     H.check(lib.rdn_sqnorm_scaled(fp.gflat.data_ptr(), fp.numel, float(max_norm), float(pre_scale), ws.data_ptr(),
                                   fp._clip_out.data_ptr(), st), "sqnorm")
     H.check(lib.rdn_clip_scale(fp.gflat.data_ptr(), fp.numel, fp._clip_out[1:].data_ptr(), st), "clip_scale")
-    return fp._clip_out[0].clone()
+    return fp._clip_out[0].clone() if want_norm else None
 
 
-def clip_grad_norm_(parameters, max_norm, norm_type=2.0):
+def clip_grad_norm_(parameters, max_norm, norm_type=2.0, want_norm=True):
     """torch.nn.utils.clip_grad_norm_ drop-in: the fused flat path when the
     parameters are one fused network's, torch's own otherwise."""
     if isinstance(parameters, torch.Tensor):
@@ -134,7 +136,7 @@ def clip_grad_norm_(parameters, max_norm, norm_type=2.0):
     parameters = list(parameters)
     fp = find_flat(parameters) if norm_type == 2.0 else None
     if fp is not None:
-        return clip_grad_norm_flat(fp, max_norm)
+        return clip_grad_norm_flat(fp, max_norm, want_norm=want_norm)
     return torch.nn.utils.clip_grad_norm_(parameters, max_norm, norm_type)
 
 
