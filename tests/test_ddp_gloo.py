@@ -60,13 +60,15 @@ def test_plan_buckets_small_tail():
     assert b[-1][0] == 0 and 0 < b[-1][1] <= 80000 and b[-1][1] in fp.offsets
 
 
-def _worker(rank, world, init_file, q, defer=False):
+def _worker(rank, world, init_file, q, defer=False, bucket_mb=0.4, tail_mb=4.0):
     # file:// rendezvous: no TCP port to race for between parallel test runs
     dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
     try:
         fp = _fake_flat(100 + rank, SIZES)
         mine = fp.gflat.clone()
-        gs = GradSync(fp, bucket_mb=0.4, overlap=False)
+        gs = GradSync(fp, bucket_mb=bucket_mb, overlap=False, tail_mb=tail_mb)
+        if tail_mb < 1.0:   # the start bucket split off small (ddp.plan_buckets tail_elems)
+            assert len(gs.buckets) == 3 and gs.buckets[-1][0] == 0, gs.buckets
         gs.defer_average = defer
         gs.begin()
         # backward order: parameters complete from the last to the first, in groups of 3
@@ -93,12 +95,13 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("defer", [False, True], ids=["average", "deferred"])
-def test_gradsync_world2_gloo_average(tmp_path, defer):
+@pytest.mark.parametrize("defer,bucket_mb,tail_mb", [(False, 0.4, 4.0), (True, 0.4, 4.0), (False, 4.0, 0.3)],
+                         ids=["average", "deferred", "small-tail"])
+def test_gradsync_world2_gloo_average(tmp_path, defer, bucket_mb, tail_mb):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     init_file = str(tmp_path / "rendezvous")
-    procs = [ctx.Process(target=_worker, args=(r, 2, init_file, q, defer)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, init_file, q, defer, bucket_mb, tail_mb)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict()
