@@ -577,12 +577,19 @@ Plan plan(const rdn_wgrad_desc* d) {
     p.mtiles = (d->mdim + p.bm - 1) / p.bm;
     p.chunks = d->ndim / p.ck;
     const int base = p.mtiles * p.chunks;
-    // blocks per launch: 192 of the 256 CUs, leaving room beside the dgrad chain;
+    // blocks per launch: 128 of the 256 CUs, leaving room beside the dgrad chain;
     // step A/B (3 interleaved rounds, same box): 128: 1483, 192: 1506, 256: 1499,
     // 512: 1416 img/s (past 256 the 1-per-CU blocks run in two waves); re-measured in
     // r03 (profiles/r03_v10_wglds_blocks_ab.txt): 96: 1633, 128: 1698, 160: 1714,
-    // 192: 1714, 256: 1687
-    constexpr int gtarget = 192;
+    // 192: 1714, 256: 1687; round 4, after the fused layers' work moved onto the
+    // compute stream (gate-out, batched reduce): 192: 1767 / 1991, 160: 1777 / 1997,
+    // 128: 1777 / 2011 img/s B16 / B32, then 128: 1764 / 1975, 112: 1759 / 1957,
+    // 96: 1730 / 1927 (profiles/r04_v28_wglds_blocks_ab.txt, r04_v29_*).  RDN_WGLDS_BLOCKS
+    static const int gtarget = [] {
+      const char* e = getenv("RDN_WGLDS_BLOCKS");
+      const int v = e ? atoi(e) : 0;
+      return v > 0 ? v : 128;
+    }();
     int s = d->splits > 0 ? d->splits : gtarget / base;
     const int maxs = (p.ntiles + 1) / 2;                             // >= 2 tiles per block
     if (s > maxs) s = maxs;
