@@ -18,6 +18,8 @@
 // ds_read_b32 per lane (v_mfma_f32_16x16x4_f32 takes one k per lane group).
 #include "rdn_common.h"
 
+#include <cstdlib>
+
 namespace {
 
 constexpr int NT = 256;
@@ -299,7 +301,14 @@ static int auto_splits(const rdn_wgrad_desc* d) {
   const int taps = d->gather == RDN_G_CONV3 ? 9 : 4;
   const int64_t tiles = (int64_t)((d->mdim + c.bm - 1) / c.bm) * ((taps * d->ndim + c.bn - 1) / c.bn);
   const int64_t P = (int64_t)d->n * d->h * d->w;
-  int64_t s = (512 + tiles - 1) / tiles;                  // ~2 blocks per CU
+  // ~2 blocks per CU (round 4, interleaved: 512 1771 / 1957, 256 1765 / 1939, 128 1767 /
+  // 1941 img/s B16 / B32, profiles/r04_v31_wg2_blocks_ab.txt; RDN_WG2_BLOCKS for A/B)
+  static const int64_t target = [] {
+    const char* e = getenv("RDN_WG2_BLOCKS");
+    const int v = e ? atoi(e) : 0;
+    return (int64_t)(v > 0 ? v : 512);
+  }();
+  int64_t s = (target + tiles - 1) / tiles;
   const int64_t maxs = (P + 1023) / 1024;                 // >= 1024 pixels per split
   if (s > maxs) s = maxs;
   if (s < 1) s = 1;
