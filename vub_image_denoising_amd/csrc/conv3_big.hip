@@ -113,8 +113,11 @@ __device__ __forceinline__ void wait_split(int wave) {   // vmcnt(wave < SPLIT ?
 
 // launch bounds: 512 threads = 8 waves = two per SIMD, i.e. one block per CU (the LDS
 // budget allows no more); the second argument is waves per SIMD (EU), so the register
-// cap it implies is 256 VGPRs per lane, which every instantiation fits without spill
-// (hipcc -Rpass-analysis / .vgpr_count, round 4: 116-247)
+// cap it implies is 256 VGPRs per lane (the most a 512-thread block can have; a bound of
+// 1 would not raise it).  Round-4 end, -Rpass-analysis=kernel-resource-usage
+// (profiles/r04_final_conv3_big_resources.txt): 139-251 VGPRs, no scratch, except the
+// 128-column CK=64 items at 253-255 VGPRs, four of which (EP=1; EP=2..4 with GO) spill
+// 20-36 B/lane -- the next register cut is there (a 128-column wave tile split)
 template <int TH, int BN, int WM, int CK, int EP, bool GO>
 __global__ __launch_bounds__(NTB, 2) void conv3_big_kernel(rdn_conv_desc d, int tiles_x, int tiles_y, int nitems) {
   using Cfg = PtCfg<TH, BN, WM, CK>;
