@@ -53,10 +53,25 @@ def main():
                     out.append(f"  {c}/WAVE = {avg[c] / wc:.3f}")
         if "TCP_TCC_READ_REQ_sum" in avg and avg["TCP_TCC_READ_REQ_sum"]:
             out.append(f"  L1->L2 read latency = {avg['TCP_TCC_READ_REQ_LATENCY_sum'] / avg['TCP_TCC_READ_REQ_sum']:.0f} cyc")
+        # MFMA pipe utilisation over the dispatch (1024 SIMDs; GRBM_GUI_ACTIVE sums the
+        # 8 XCDs' cycles: /8 = the dispatch's cycles, MI355X_MICROARCH.md DVFS note)
+        gui = avg.get("GRBM_GUI_ACTIVE")
+        if gui:
+            cyc = gui / 8.0
+            d_us = sum(dur[k]) / max(1, len(dur[k]))
+            out.append(f"  clock ~ {cyc / d_us / 1e3:.2f} GHz")
+            if "SQ_VALU_MFMA_BUSY_CYCLES" in avg:
+                out.append(f"  MFMA busy = {avg['SQ_VALU_MFMA_BUSY_CYCLES'] / (1024 * cyc):.3f} of the SIMD cycles")
+            if "SQ_INSTS_MFMA" in avg:
+                out.append(f"  MFMA issue (x16 cyc, 16x16x32) = {16 * avg['SQ_INSTS_MFMA'] / (1024 * cyc):.3f}")
+        if avg.get("SQ_LDS_IDX_ACTIVE"):
+            out.append(f"  LDS bank-conflict cycles / LDS cycles = "
+                       f"{avg.get('SQ_LDS_BANK_CONFLICT', 0) / avg['SQ_LDS_IDX_ACTIVE']:.3f}")
         waves = avg.get("SQ_WAVES") or None
         for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_MFMA", "SQ_INSTS_VMEM_RD",
                   "SQ_INSTS_VMEM_WR", "SQ_INST_LEVEL_VMEM", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS",
-                  "SQ_ACTIVE_INST_VMEM", "SQ_LDS_BANK_CONFLICT", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CYCLES",
+                  "SQ_ACTIVE_INST_VMEM", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", "SQ_WAIT_INST_LDS",
+                  "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CYCLES",
                   "GRBM_GUI_ACTIVE"):
             if c in avg:
                 out.append(f"  {c} = {avg[c]:.4g}")

@@ -10,8 +10,11 @@ kernel's ranges), i.e. by fp32 summation order: rel-L2 <= 1e-5 per tensor (measu
 on MI355X below 1e-6).  Network: RDUNet_T (Unet_model.py:133-166) in bf16 at a
 full 256-wide level 0 and at small sizes, where the ragged XCD tile ranges leave
 some blocks without tiles (zero slabs).  The level-1 conv_1 / conv_2 run as column
-halves (two blocks per tile, 48 / 64 of their 96 / 128 input channels each) against
-the gated-free separate path (PReLU-backward pass, conv3_big dgrad, wgrad3_glds).
+halves (two blocks per tile, 48 / 64 of their 96 / 128 input channels each) and the
+level-1 conv_3 as five 32-channel parts (round 5; pre-gated: it reads the dYpre of the
+PReLU-backward pass) against the gated-free separate path (PReLU-backward pass,
+conv3_big dgrad, wgrad3_glds).  The five-part kernel gated in its own loaders
+(RDN_DW_PREGATED=0) is checked against the pre-gated one below.
 The gate-out epilogue (test_gpu_gateout.py) is off on both sides: a conv that runs
 fused here cannot finish another layer's PReLU backward, so with it on the two sides
 would pair different layers with it and differ by bf16 rounding noise, which is
@@ -62,9 +65,36 @@ def test_fused_dgrad_wgrad_matches_separate(B, S):
     assert n1 and all(k.startswith("conv3_dw_kernel") for k in n1), n1
     if S >= 64:   # level-1 conv_1 / conv_2 (96 / 128 input channels) in column halves
         assert any(k.endswith(",h2>") for k in n1), n1
+        # level-1 conv_3 (160 input channels, 64 dY channels): five 32-channel parts
+        assert any(",64,h5" in k for k in n1), n1
     assert torch.equal(y0, y1)
     worst = max(_rel(g1[k], g0[k]) for k in g0)
     assert worst <= 1e-5, sorted(((_rel(g1[k], g0[k]), k) for k in g0), reverse=True)[:5]
     # activation gradients are bit-identical: the first conv's weight gradient
     # (input block, level 0, no gate: separate kernels on both sides) sees them
     assert torch.equal(g1["input_block.conv_1.weight"], g0["input_block.conv_1.weight"])
+
+
+@pytest.mark.parametrize("B,S", [(2, 256), (2, 64)])
+def test_level1_conv3_gated_vs_pregated(B, S):
+    """The level-1 conv_3's five-part fused kernel gating dY in its loaders against
+    the same kernel reading the PReLU-backward pass's dYpre: the same bf16 dYpre
+    operand either way, so every conv weight and activation gradient is bit-identical;
+    the PReLU-slope / bias gradients differ by fp32 summation order only."""
+    from vub_image_denoising_amd import engine as E
+    old = E.DW_PREGATED
+    try:
+        E.DW_PREGATED = True
+        y0, g0, n0 = _grads(True, B, S)
+        E.DW_PREGATED = False
+        y1, g1, n1 = _grads(True, B, S)
+    finally:
+        E.DW_PREGATED = old
+    assert any(k.endswith(",64,h5,pregated>") for k in n0), n0
+    assert any(k.endswith(",64,h5>") for k in n1), n1
+    assert torch.equal(y0, y1)
+    for n in g0:
+        if ".conv" in n and n.endswith(".weight"):
+            assert torch.equal(g1[n], g0[n]), (n, _rel(g1[n], g0[n]))
+    worst = max(_rel(g1[k], g0[k]) for k in g0)
+    assert worst <= 1e-5, sorted(((_rel(g1[k], g0[k]), k) for k in g0), reverse=True)[:5]

@@ -26,6 +26,18 @@ def _rel(a, b):
     return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
 
 
+def DW_PREGATED():
+    from vub_image_denoising_amd import engine as E
+    return E.DW_PREGATED
+
+
+_LAST_DW = {}
+
+
+def _dw_keys(S):
+    return _LAST_DW.get(S, [])
+
+
 def _grads(gate_out, dtype, B, S, F0=32, seed=0):
     import vub_image_denoising_amd as vm
     from vub_image_denoising_amd import engine as E
@@ -43,9 +55,12 @@ def _grads(gate_out, dtype, B, S, F0=32, seed=0):
         (y * w).mean().backward()
         grads = {n: p.grad.detach().clone() for n, p in m.named_parameters()}
         keys = []
+        _LAST_DW[S] = []
         for pool in m._rdn_engines.values():
             for eng in pool:
                 for L in eng.layers:
+                    if "dw" in L.extra.get("info", {}):
+                        _LAST_DW.setdefault(S, []).append((L.name, L.extra["info"]["dw"][2]))
                     if L.extra.get("gates") is not None:
                         info = L.extra["info"]
                         keys.append((L.name, L.extra["gates"].name, info["dw"][2] if "dw" in info else info["dgrad"][2]))
@@ -85,10 +100,14 @@ def test_gate_out_bf16_matches_separate(B, S):
     if S >= 64:   # the fused dgrad+wgrad finishers (conv3_dw ",go"): up_0.conv finishes
         # up_0.conv_t; a level-1 block's conv_0 finishes the layer feeding the block
         # (encoder block_1_1 <- block_1_0.conv_3; decoder block_1_2 <- up_1.conv,
-        # block_1_3 <- block_1_2.conv_3; block_1_0's input is down_0's, a 2x2 conv: not here)
+        # block_1_3 <- block_1_2.conv_3; block_1_0's input is down_0's, a 2x2 conv: not here;
+        # since round 5 the finished conv_3s run the pre-gated fused dgrad+wgrad, ",pregated")
         fin = {(j, k) for j, k, key in k1 if key.startswith("conv3_dw") and ",go" in key}
         assert fin == {("up_0.conv", "up_0.conv_t"), ("block_1_1.conv_0", "block_1_0.conv_3"),
                        ("block_1_2.conv_0", "up_1.conv"), ("block_1_3.conv_0", "block_1_2.conv_3")}, k1
+        if DW_PREGATED():   # the finished level-1 conv_3s read the dYpre these epilogues write
+            pre = {L for L, key in _dw_keys(S) if key.endswith(",pregated>")}
+            assert {"block_1_0.conv_3", "block_1_2.conv_3"} <= pre, pre
     if B == 16:   # the train step's shape: conv3_big serves the level-1 and up-conv finishers
         assert any("conv3_big" in k and ",go" in k for _, _, k in k1), k1
         assert any("conv3_halo" in k for _, _, k in k1), k1

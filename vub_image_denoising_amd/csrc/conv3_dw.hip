@@ -118,12 +118,16 @@ struct DwCfg {
   // (96 columns were tried: <96,32> spills 128 B in the W loop, so they stay on the
   // separate kernels)
   static constexpr int XB = SB ? 2 : DW2 ? 1 : (BASE + 2 * X_BYTES <= LDS_MAX ? 2 : 1);
-  static constexpr int LDS = BASE + XB * X_BYTES;
+  // 16 B per thread of a role: the padding units of the last halo load round store
+  // here instead of skipping their store (a lane-divergent skip made hipcc wait
+  // vmcnt(0) at the loop head, i.e. on the previous tile's dX stores)
+  static constexpr int DUMP_BYTES = 256 * 16;
+  static constexpr int LDS = BASE + XB * X_BYTES + DUMP_BYTES;
   static constexpr bool FITS = LDS <= LDS_MAX && D_BYTES + X_BYTES + CT_BYTES >= RED_BYTES &&
                               (!GO || W_BYTES >= 8 * BN * 4);   // gate-out partials in the dead panel
 };
 
-template <int BN, int CK, int NH, bool GO>
+template <int BN, int CK, int NH, bool GO, bool GT>
 __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wgrad_desc wg, int tiles_x, int tiles_y,
                                                          int ntiles) {
   using Cfg = DwCfg<BN, CK, GO>;
@@ -152,6 +156,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
   unsigned char* const dyh = lds + Cfg::W_BYTES;
   unsigned char* const xh = dyh + Cfg::DB * Cfg::D_BYTES;
   float* const alds = (float*)(xh + Cfg::XB * Cfg::X_BYTES + Cfg::CT_BYTES);
+  unsigned char* const dump = lds + Cfg::LDS - Cfg::DUMP_BYTES;
   float* const galds = alds + Cfg::AL_BYTES / 4;        // (GO) slopes of the finished layer, this half's columns
   float* const gred = (float*)lds;                      // (GO) its partials, [D wave][2][BN] over the dead panel
   float* const red = (float*)(lds + Cfg::W_BYTES);   // partial reduction (aliases the halos after the loops)
@@ -189,7 +194,8 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       const int n = u / UPRW, k8 = u - n * UPRW;
       *(u32x4*)(wl + n * WROW + k8 * 16) = *(const u32x4*)(WP + (int64_t)(col0 + n) * d.kp + k8 * VEC);
     }
-    for (int c = tid; c < CK; c += NT) alds[c] = d.gate_alpha[c];
+    if constexpr (GT)
+      for (int c = tid; c < CK; c += NT) alds[c] = d.gate_alpha[c];
     if constexpr (GO) {
       for (int c = tid; c < BN; c += NT) {
         const int gc = col0 + c - d.gout_c0;
@@ -273,7 +279,8 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       int oy, ox, on;
       origin(tt, oy, ox, on);
       const int64_t hpix0 = ((int64_t)on * H + (oy - 1)) * W + (ox - 1);
-      const __amdgpu_buffer_rsrc_t rd = rdn_rsrc(DY + hpix0 * d.x_ps), rg = rdn_rsrc(PR + hpix0 * d.gate_ps);
+      const __amdgpu_buffer_rsrc_t rd = rdn_rsrc(DY + hpix0 * d.x_ps);
+      const __amdgpu_buffer_rsrc_t rg = rdn_rsrc(GT ? PR + hpix0 * d.gate_ps : DY);
 #pragma unroll
       for (int it = 0; it < D_IT; ++it) {
         const bool ok = in_img(uhp[it], oy, ox);
@@ -283,21 +290,51 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
         (void)rd; (void)rg;
 #else
         lr[it] = rdn_ld16(rd, ok, lrel[it] * 2);
-        gr[it] = rdn_ld16(rg, ok, grel[it] * 2);
+        if constexpr (GT) gr[it] = rdn_ld16(rg, ok, grel[it] * 2);
+        else gr[it] = u32x4{0u, 0u, 0u, 0u};
 #endif
       }
     };
     // registers -> LDS with the PReLU-backward gate and the dalpha/dbias partials of
     // the tile-interior pixels (each image pixel is interior to exactly one tile)
     auto store = [&](const u32x4 (&lr)[D_IT], const u32x4 (&gr)[D_IT], bool live, int doff) {
+      if constexpr (!GT) {   // the operand is dYpre already (gate-out finisher / PReLU pass)
+#pragma unroll
+        for (int it = 0; it < D_IT; ++it)
+          *(u32x4*)(uhp[it] < HW_ ? dyh + doff + llds[it] : dump + rt * 16) = lr[it];
+        return;
+      }
       const f32x4 a0 = *(const f32x4*)(alds + dcu * VEC), a1 = *(const f32x4*)(alds + dcu * VEC + 4);
+#if !defined(DW_DIAG_NO_GATE) && !defined(DW_SLOW_GATE)
+#ifdef DW_DIAG_FAST_ALL   // diagnostic build: every block gates without counting partials
+      if (true) {
+#else
+      if (!live) {   // (block-uniform) no partials to count: the packed gate, ~half the VALU
+#endif
+#pragma unroll
+        for (int it = 0; it < D_IT; ++it) {
+          u32x4 o;
+          o[0] = rdn_gate2(lr[it][0], gr[it][0], a0[0], a0[1]);
+          o[1] = rdn_gate2(lr[it][1], gr[it][1], a0[2], a0[3]);
+          o[2] = rdn_gate2(lr[it][2], gr[it][2], a1[0], a1[1]);
+          o[3] = rdn_gate2(lr[it][3], gr[it][3], a1[2], a1[3]);
+          *(u32x4*)(uhp[it] < HW_ ? dyh + doff + llds[it] : dump + rt * 16) = o;
+        }
+        return;
+      }
+#endif
 #pragma unroll
       for (int it = 0; it < D_IT; ++it) {
-        if (uhp[it] >= HW_) continue;
         float dy[VEC], pr[VEC];
         Unit16<bf16>::unpack(lr[it], dy);
         Unit16<bf16>::unpack(gr[it], pr);
         const bool in = live && ((dint >> it) & 1u);   // a re-read past the range counts nothing
+        unsigned char* const dst = uhp[it] < HW_ ? dyh + doff + llds[it] : dump + rt * 16;
+#ifdef DW_DIAG_NO_GATE   // diagnostic build: the raw dY goes to LDS (no gate, no partials)
+        (void)in; (void)a0; (void)a1;
+        *(u32x4*)dst = lr[it];
+        continue;
+#endif
 #pragma unroll
         for (int q = 0; q < VEC; ++q) {
           const bool pos = pr[q] > 0.f;
@@ -305,7 +342,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
           dy[q] = pos ? dy[q] : (q < 4 ? a0[q] : a1[q - 4]) * dy[q];
           if (in) sb[q] += dy[q];
         }
-        *(u32x4*)(dyh + doff + llds[it]) = Unit16<bf16>::pack(dy);
+        *(u32x4*)dst = Unit16<bf16>::pack(dy);
       }
     };
     auto load_epi = [&](int tt, u32x2 (&eo)[MT][NE]) {
@@ -456,9 +493,10 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     // register sets in flight measured no faster and spill the 80-column shape)
     if (t < t_hi) {
       load(t, lA, gA);
-      load_epi(t, eC);
       store(lA, gA, half == 0, 0);
       load(min(t + per, t_last), lA, gA);
+      load_epi(t, eC);   // (after the halo, as in the loop: the loop head's vmcnt waits then
+                         // count the same ops on entry and on the back edge, not vmcnt(0))
     }
     __syncthreads();   // weights + first halos
     auto step = [&](u32x4 (&lc)[D_IT], u32x4 (&gc)[D_IT], const u32x2 (&ec)[MT][NE], u32x2 (&en)[MT][NE],
@@ -477,8 +515,8 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     } else {
     if (t < t_hi) {
       load(t, lA, gA);
-      load_epi(t, eC);
       store(lA, gA, half == 0, 0);
+      load_epi(t, eC);
       load(min(t + per, t_last), lA, gA);
     }
     __syncthreads();   // weights + first halos
@@ -520,7 +558,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
           }
       }
     }
-    if (wg.part) {
+    if (GT && wg.part) {
 #pragma unroll
       for (int k = 0; k < VEC; ++k) {
         red[rt * VEC + k] = sa[k];
@@ -560,7 +598,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     auto store = [&](const u32x4 (&lr)[X_IT], int xoff) {
 #pragma unroll
       for (int it = 0; it < X_IT; ++it)
-        if (llds[it] >= 0) *(u32x4*)(xh + xoff + llds[it]) = lr[it];
+        *(u32x4*)(llds[it] >= 0 ? xh + xoff + llds[it] : dump + rt * 16) = lr[it];
     };
     // lane (g, q = r>>2, pp = r&3) supplies pixels {4g+q, 16+4g+q} of each 32-pixel
     // k-step (tile rows 2ks, 2ks+1) and channels / columns 4pp..4pp+3
@@ -763,7 +801,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
   // dalpha / dbias partials of this split, fixed order.  Both roles arrive at this
   // ONE barrier (each role's loop passes the same number of barriers per tile), so
   // no barrier is ever role-divergent.
-  if (wg.part) {
+  if (GT && wg.part) {
     __syncthreads();
     if (dwave && rt < CK) {
       constexpr int DUC = CK / VEC;
@@ -838,7 +876,14 @@ bool dw_halves_enabled() {
   return on;
 }
 int dw_nh(const rdn_conv_desc* d) {
-  return (dw_halves_enabled() && d->cin == 32 && (d->ncols == 96 || d->ncols == 128)) ? 2 : 1;
+  if (!dw_halves_enabled()) return 1;
+  if (d->cin == 32 && (d->ncols == 96 || d->ncols == 128)) return 2;
+  static const bool h5 = [] {   // (RDN_DW_H5=0: the level-1 conv_3 on the separate kernels, for A/B)
+    const char* e = getenv("RDN_DW_H5");
+    return !(e && e[0] == '0');
+  }();
+  if (h5 && d->cin == 64 && d->ncols == 160) return 5;   // level-1 conv_3: five 32-channel parts
+  return 1;
 }
 
 // gate-out (d->gout) on this pair: the instantiated shapes (up_0.conv: 96 columns in
@@ -858,13 +903,18 @@ bool dw_gout_ok(const rdn_conv_desc* d, const rdn_wgrad_desc* wg) {
 bool dw_serves(const rdn_conv_desc* d, const rdn_wgrad_desc* wg) {
   if (!dw_enabled() || !d || !wg) return false;
   if (d->dtype != RDN_BF16 || wg->dtype != RDN_BF16 || d->gather != RDN_G_CONV3 || wg->gather != RDN_G_CONV3) return false;
-  if (!d->gate || !wg->a_gate || !d->gate_alpha || d->bn || d->bm) return false;
+  if (d->bn || d->bm) return false;
+  // gated (the loaders apply the PReLU backward, dalpha/dbias partials in wg->part) or,
+  // for the level-1 conv_3 only, pre-gated: the operand is the layer's dYpre (written
+  // by a gate-out finisher or the PReLU-backward pass, which also count the partials)
+  const bool gated = d->gate && wg->a_gate && d->gate_alpha;
+  if (!gated && (d->gate || wg->a_gate || wg->part || !(d->cin == 64 && d->ncols == 160))) return false;
   if (d->gout && !dw_gout_ok(d, wg)) return false;
   if (d->flags & ~(RDN_EPI_RESID | RDN_EPI_ACCUM | (d->gout ? RDN_EPI_GOUT_KEEP : 0))) return false;
   if ((d->flags & RDN_EPI_RESID) && (d->flags & RDN_EPI_ACCUM)) return false;
   if (d->h % TH || d->w % TW || d->n != wg->n || d->h != wg->h || d->w != wg->w) return false;
-  if (d->cin != 16 && d->cin != 32) return false;
   const int nh = dw_nh(d);
+  if (d->cin != 16 && d->cin != 32 && !(d->cin == 64 && nh == 5)) return false;
   if (d->ncols != d->cout || d->ncols % 16 || d->ncols < 32 || d->ncols / nh > 80 || wg->ndim != d->ncols) return false;
   if (wg->mdim > d->cin || wg->mdim <= 0 || wg->b_c0 % 8 || wg->b_ps % 8 || ((uintptr_t)wg->b & 15)) return false;
   // the same gated operand on both sides
@@ -891,7 +941,7 @@ bool dw_serves(const rdn_conv_desc* d, const rdn_wgrad_desc* wg) {
   return nt < (1ll << 31);
 }
 
-template <int BN, int CK, int NH = 1, bool GO = false>
+template <int BN, int CK, int NH = 1, bool GO = false, bool GT = true>
 int launch_dw(const rdn_conv_desc* d, const rdn_wgrad_desc* wg, hipStream_t st) {
   if constexpr (!DwCfg<BN, CK, GO>::FITS) {
     return 1;
@@ -899,6 +949,7 @@ int launch_dw(const rdn_conv_desc* d, const rdn_wgrad_desc* wg, hipStream_t st) 
     const int tiles_x = d->w / TW, tiles_y = d->h / TH;
     const int ntiles = d->n * tiles_x * tiles_y;
     const int grid = dw_grid(ntiles, NH);
+    if (!GT) RDN_PROBE("conv3_dw_kernel<bf16,%d,%d,h%d,pregated>", BN, CK, NH);
     if (NH > 1) RDN_PROBE("conv3_dw_kernel<bf16,%d,%d,h%d%s>", BN, CK, NH, GO ? ",go" : "");
     RDN_PROBE("conv3_dw_kernel<bf16,%d,%d%s>", BN, CK, GO ? ",go" : "");
     if (wg->splits != grid) {
@@ -906,7 +957,7 @@ int launch_dw(const rdn_conv_desc* d, const rdn_wgrad_desc* wg, hipStream_t st) 
       return RDN_E_ARG;
     }
     if (!wg->ws) { rdn_set_error("rdn_conv_dgrad_wgrad: null workspace"); return RDN_E_ARG; }
-    hipLaunchKernelGGL((conv3_dw_kernel<BN, CK, NH, GO>), dim3((unsigned)grid), dim3(NT), 0, st, *d, *wg, tiles_x,
+    hipLaunchKernelGGL((conv3_dw_kernel<BN, CK, NH, GO, GT>), dim3((unsigned)grid), dim3(NT), 0, st, *d, *wg, tiles_x,
                        tiles_y, ntiles);
     return rdn_check_launch("rdn_conv_dgrad_wgrad");
   }
@@ -914,6 +965,11 @@ int launch_dw(const rdn_conv_desc* d, const rdn_wgrad_desc* wg, hipStream_t st) 
 
 template <int CK>
 int dw_bn(const rdn_conv_desc* d, const rdn_wgrad_desc* wg, hipStream_t st) {
+  if constexpr (CK == 64) {   // (dw_serves: the level-1 conv_3, 160 input channels in five parts)
+    if (!d->gout && dw_nh(d) == 5 && d->ncols == 160)
+      return d->gate ? launch_dw<32, 64, 5>(d, wg, st) : launch_dw<32, 64, 5, false, false>(d, wg, st);
+    return 1;
+  } else {
   if (d->gout) {   // (dw_gout_ok: these two shapes only)
     if constexpr (CK == 32) {
       if (d->ncols == 96) return launch_dw<48, 32, 2, true>(d, wg, st);
@@ -937,11 +993,12 @@ int dw_bn(const rdn_conv_desc* d, const rdn_wgrad_desc* wg, hipStream_t st) {
     case 80: return launch_dw<80, CK>(d, wg, st);
   }
   return 1;
+  }
 }
 
 int dw_dispatch(const rdn_conv_desc* d, const rdn_wgrad_desc* wg, hipStream_t st) {
   if (!dw_serves(d, wg)) return 1;
-  return d->cin == 32 ? dw_bn<32>(d, wg, st) : dw_bn<16>(d, wg, st);
+  return d->cin == 64 ? dw_bn<64>(d, wg, st) : d->cin == 32 ? dw_bn<32>(d, wg, st) : dw_bn<16>(d, wg, st);
 }
 
 }  // namespace

@@ -115,6 +115,24 @@ __device__ __forceinline__ u32x2 rdn_pack4(const float* f) {
   return u;
 }
 
+// PReLU backward of two bf16 channels packed in a dword (aten _prelu_kernel_backward
+// with a bf16 output): dYpre = pre > 0 ? dY : bf16(alpha * dY).  `pre > 0` from the
+// bf16 bit pattern b, per 16-bit half: (u16)(b - 1) < 0x7F80 -- +0, -0, negatives
+// and NaN take the slope branch, exactly as the fp32 compare does -- as the sign of
+// sat_u16((b - 1) + 0x80), spread to a 16-bit mask by an arithmetic shift (inline
+// asm: hipcc turns the vector form back into per-half compares and selects).  The
+// positive halves keep dY's bits; the others are the RNE-rounded product.
+__device__ __forceinline__ unsigned rdn_gate2(unsigned dy, unsigned pre, float alo, float ahi) {
+  unsigned m;
+  asm("v_pk_sub_u16 %0, %1, %2\n\tv_pk_add_u16 %0, %0, %3 clamp\n\tv_pk_ashrrev_i16 %0, %4, %0"
+      : "=&v"(m)
+      : "v"(pre), "s"(0x00010001u), "s"(0x00800080u), "s"(0x000f000fu));
+  const float lo = __builtin_bit_cast(float, dy << 16) * alo, hi = __builtin_bit_cast(float, dy & 0xffff0000u) * ahi;
+  const unsigned g = (unsigned)__builtin_bit_cast(unsigned short, (bf16)lo) |
+                     ((unsigned)__builtin_bit_cast(unsigned short, (bf16)hi) << 16);
+  return (g & m) | (dy & ~m);
+}
+
 // Fast unsigned division by a runtime-invariant divisor (n < 2^31).
 struct FastDiv {
   uint32_t d, m, s;

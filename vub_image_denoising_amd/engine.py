@@ -226,6 +226,13 @@ GATE_OUT = os.environ.get("RDN_GATE_OUT", "1") == "1"
 # gate-out in the fused dgrad+wgrad kernel (conv3_dw ",go": up_0.conv finishing
 # up_0.conv_t, the level-1 conv_0s finishing down_0 / the previous block's conv_3)
 GATE_OUT_DW = os.environ.get("RDN_GATE_OUT_DW", "1") == "1"
+# round 5: the level-1 conv_3 (160 input channels, 64 dY channels) as ONE fused dgrad +
+# wgrad launch in five 32-channel parts (conv3_dw "h5") instead of conv3_big dgrad on
+# the compute stream + wgrad3_glds on the side stream.  Pre-gated: the kernel reads the
+# layer's dYpre, gated once by a gate-out finisher or the PReLU-backward pass (gated in
+# each part's loader, the five parts gated the same tile five times: 143 vs 101 us per
+# launch at B16, profiles/r05_*); RDN_DW_PREGATED=0 gates in the loaders instead
+DW_PREGATED = os.environ.get("RDN_DW_PREGATED", "1") != "0"
 # the fused layers' split-K reduces of consecutive fused layers in one launch
 # (rdn_wgrad_reduce_batch; RDN_REDUCE_BATCH=0: one launch per layer)
 REDUCE_BATCH = os.environ.get("RDN_REDUCE_BATCH", "1") != "0"
@@ -853,7 +860,11 @@ class UNetEngine:
 
             d, wg, taps, ndim_real = build(fused)
             dw = 0
-            if gate_ok and FUSE_DW and not pure:
+            pregated = False
+            if gate_ok and FUSE_DW and not pure and not fused and DW_PREGATED:
+                # the pre-gated fused kernel (dYpre from the PReLU pass / a gate-out finisher)
+                pregated = lib.rdn_conv_dgrad_wgrad_splits(C.byref(d), C.byref(wg)) > 0
+            if gate_ok and FUSE_DW and not pure and not pregated:
                 # the fused dgrad + wgrad kernel gates in its own loader, also for the
                 # multi-chunk level-1 convs (column halves, rdn_conv_dgrad_wgrad_cols)
                 dg, wgg, _, _ = (d, wg, taps, ndim_real) if fused else build(True)
@@ -868,7 +879,7 @@ class UNetEngine:
             splits = lib.rdn_wgrad_splits(C.byref(wg))
             wg.splits = splits
             dw = 0
-            if fused and FUSE_DW and L.src.buf not in self.pure_inputs:
+            if (fused or pregated) and FUSE_DW and L.src.buf not in self.pure_inputs:
                 dw = lib.rdn_conv_dgrad_wgrad_splits(C.byref(d), C.byref(wg))
             L.extra["dw"] = dw > 0
             L.extra["dw_bytes"] = 0
@@ -1282,7 +1293,7 @@ class UNetEngine:
                         part=pws if hh == 0 else None, dalpha=gbase + oa, dbias=gbase + ob,
                         splits=sh, mdim=mdim, ndim=cols if nh > 1 else ndim, ndim_real=cols if nh > 1 else ndim_real,
                         taps=taps, gstride=ndim_real, gci0=hh * cols, accumulate=1,
-                        part_splits=sh if nh > 1 else part_splits))
+                        part_splits=sh if (nh > 1 and fused) else part_splits))
                 pending.append((L, jobs))
                 continue
             if cols < ndim:
@@ -1292,7 +1303,8 @@ class UNetEngine:
                 for hh in range(nh):
                     rc = lib.rdn_wgrad_reduce_cols(L.wgrad_desc.ws + hh * sh * mdim * taps * cols * 4, sh, mdim, cols,
                                                    taps, gbase + ow, ndim_real, hh * cols, 1,
-                                                   pws if hh == 0 else None, sh, gbase + oa, gbase + ob, rst)
+                                                   pws if hh == 0 else None, sh if fused else part_splits,
+                                                   gbase + oa, gbase + ob, rst)
                     if rc:
                         break
             else:
