@@ -509,34 +509,80 @@ def _free_port():
     return port
 
 
-def _run_ranks(n, argv, grace_s=60.0):
+# a rank that outlives the deadline (every rank hung in a collective, say) is killed
+# and the job exits with this code, so a caller's clock never runs out on a silent run
+EXIT_DEADLINE = 124
+
+
+def deadline_s(args):
+    """Wall-clock budget of one rank / one launch: `--deadline-s`, else a bound
+    derived from the work (start-up, capture and profiling passes, the B32 / fp32
+    lines and CPU legs of a 1-GPU run, 4 s per timed or warm-up step)."""
+    if args.deadline_s and args.deadline_s > 0:
+        return float(args.deadline_s)
+    return 900.0 + 4.0 * (args.steps + args.warmup)
+
+
+def _run_ranks(n, argv, grace_s=60.0, deadline=None):
     """Start n ranks of this bench (fresh child processes, one per GPU: RANK /
     LOCAL_RANK / WORLD_SIZE / MASTER_* in their environment, rendezvous on
     127.0.0.1) and wait for them.  When a rank fails the others get `grace_s` to
     finish before their process groups are killed (a rank left waiting in a
-    collective would never return).  Returns the ranks' exit codes."""
+    collective would never return); past `deadline` seconds every rank still
+    running is killed and reported as EXIT_DEADLINE.  Returns the ranks' exit codes."""
     import signal
     import subprocess
     port = _free_port()
     procs = []
+    t0 = time.monotonic()
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RDN_BENCH_LAUNCHED="1")
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env,
                                       start_new_session=True))
+
+    def kill_running():
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, signal.SIGKILL)
+                except ProcessLookupError:
+                    pass
+
     failed_at = None
     while True:
         rcs = [p.poll() for p in procs]
         if all(rc is not None for rc in rcs):
             return rcs
+        if deadline is not None and time.monotonic() - t0 > deadline:
+            hung = [r for r, rc in enumerate(rcs) if rc is None]
+            _log(f"deadline of {deadline:.0f} s passed with rank(s) {hung} still running: killing them")
+            kill_running()
+            rcs = [p.wait() for p in procs]
+            return [EXIT_DEADLINE if r in hung else rc for r, rc in enumerate(rcs)]
         if failed_at is None and any(rc not in (None, 0) for rc in rcs):
             failed_at = time.monotonic()
         if failed_at is not None and time.monotonic() - failed_at > grace_s:
-            for p in procs:
-                if p.poll() is None:
-                    os.killpg(p.pid, signal.SIGKILL)
+            kill_running()
             return [p.wait() for p in procs]
         time.sleep(0.2)
+
+
+def start_watchdog(seconds, rank):
+    """Per-rank deadline under ANY launcher (torchrun included): a daemon thread
+    ends the process with EXIT_DEADLINE if it is still running after `seconds`
+    (a rank stuck inside a collective never returns to Python to notice)."""
+    import threading
+
+    def fire():
+        print(f"bench.py rank {rank}: deadline of {seconds:.0f} s passed, exiting with {EXIT_DEADLINE}",
+              file=sys.stderr, flush=True)
+        os._exit(EXIT_DEADLINE)
+
+    t = threading.Timer(seconds, fire)
+    t.daemon = True
+    t.start()
+    return t
 
 
 def launch(args, argv):
@@ -546,10 +592,12 @@ def launch(args, argv):
     `torchrun --nproc-per-node N bench.py --gpus N` does.  If a rank reports that
     the hipGraph capture of the RCCL step raised (exit EXIT_GRAPH_FAILED), the job
     runs again from fresh processes with --graph off."""
-    rcs = _run_ranks(args.gpus, argv)
+    dl = deadline_s(args)
+    rcs = _run_ranks(args.gpus, argv, deadline=dl)
     if EXIT_GRAPH_FAILED in rcs and args.graph == "on":
-        _log(f"graph capture failed on a rank (exit codes {rcs}); running the job again eagerly (--graph off)")
-        rcs = _run_ranks(args.gpus, [*argv, "--graph", "off"])
+        _log(f"graph capture or first replay failed on a rank (exit codes {rcs}); running the job again eagerly "
+             f"(--graph off)")
+        rcs = _run_ranks(args.gpus, [*argv, "--graph", "off"], deadline=dl)
     bad = [rc for rc in rcs if rc != 0]
     return bad[0] if bad else 0
 
@@ -578,6 +626,8 @@ def main():
                     help="process-group backend for N > 1 (nccl = RCCL; gloo only for eager plumbing tests)")
     ap.add_argument("--one-device", action="store_true",
                     help="every rank on cuda:0 (plumbing tests of N > 1 on a 1-GPU box; gloo, --graph off)")
+    ap.add_argument("--deadline-s", type=float, default=0.0,
+                    help="wall-clock limit per rank and per launch (0: derived from --steps / --warmup)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -589,9 +639,15 @@ def main():
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a {world}-rank run as "
               f"{args.gpus} GPUs", file=sys.stderr)
         sys.exit(2)
+    if world > 1 or args.deadline_s:
+        # (under bench.py's own launcher its deadline fires first; under torchrun this is the only one)
+        start_watchdog(deadline_s(args) + (30.0 if os.environ.get("RDN_BENCH_LAUNCHED") else 0.0), rank)
     if args.launch_dry_run:
         if os.environ.get("RDN_BENCH_DRY_GRAPH_FAIL") and args.graph == "on":   # tests of the eager restart
             sys.exit(EXIT_GRAPH_FAILED)
+        if os.environ.get("RDN_BENCH_DRY_HANG") == str(rank):   # tests of the deadline: this rank never returns
+            while True:
+                time.sleep(60)
         print(json.dumps({"rank": rank, "local_rank": local, "world_size": world, "graph": args.graph,
                           "master_addr": os.environ.get("MASTER_ADDR"), "master_port": os.environ.get("MASTER_PORT"),
                           "launched_by": "bench.py" if os.environ.get("RDN_BENCH_LAUNCHED") else "external"}),
@@ -601,30 +657,59 @@ def main():
         local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    cpu_group = None   # host-side agreement between the ranks (gloo), beside RCCL
     if world > 1:
         if args.dist_backend == "nccl":
             from vub_image_denoising_amd.ddp import capture_safe_env
             capture_safe_env()   # (RCCL inside the captured train step)
             dist.init_process_group("nccl", device_id=dev)
+            cpu_group = dist.new_group(backend="gloo")
         else:
             dist.init_process_group("gloo")
 
+    def all_ranks_ok(ok):
+        """Every rank's flag, agreed over the host-side group (never over RCCL, whose
+        state a failed capture may have left behind)."""
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=cpu_group)
+        return bool(t.item())
+
     graph = args.graph == "on" and not args.pmc_child
+    own_launcher = bool(os.environ.get("RDN_BENCH_LAUNCHED"))
+    capture_err = None
     try:
         tr = Trainer(dev, args.batch, args.size, args.base_filters, args.dtype, rank, world, graph=graph)
     except GraphCaptureError as e:
-        # the hipGraph capture of the data-parallel step raised: under this bench's own
-        # launcher the job restarts eagerly from fresh processes; under an external
-        # launcher (torchrun) this rank continues eagerly in-process
-        _log(f"rank {rank}: graph capture failed ({e.__cause__!r})")
-        if os.environ.get("RDN_BENCH_LAUNCHED"):
-            if world > 1:
-                dist.destroy_process_group()
-            sys.exit(EXIT_GRAPH_FAILED)
-        graph = False
+        capture_err = e
         tr = e.trainer
+        _log(f"rank {rank}: graph capture failed ({e.__cause__!r})")
+    if world > 1 and graph and not all_ranks_ok(capture_err is None):
+        # the hipGraph capture of the data-parallel step raised on some rank: no rank may
+        # replay alone.  Under this bench's own launcher every rank exits and the job
+        # restarts eagerly from fresh processes; under an external launcher (torchrun)
+        # every rank drops to eager steps together
+        if own_launcher:
+            dist.destroy_process_group()
+            sys.exit(EXIT_GRAPH_FAILED)
+        _log(f"rank {rank}: a rank's capture failed; every rank runs the step eagerly")
+        tr.graph = None
+    elif capture_err is not None:
+        raise capture_err
     graph = tr.graph is not None
     for i in range(args.warmup):
+        if graph and world > 1 and i == 0:
+            # the first replay of the RCCL step: a failure here ends this rank with
+            # EXIT_GRAPH_FAILED under every launcher (its peers are left inside the
+            # replay's collectives; bench's launcher restarts the job eagerly, torchrun
+            # stops the job), never a silent eager fallback in a suspect process
+            try:
+                tr.step(i)
+                torch.cuda.synchronize()
+            except Exception as e:   # noqa: BLE001
+                _log(f"rank {rank}: first replay of the captured RCCL step failed ({e!r})")
+                sys.stderr.flush()
+                os._exit(EXIT_GRAPH_FAILED)
+            continue
         tr.step(i)
     torch.cuda.synchronize()
 
@@ -644,12 +729,30 @@ def main():
     # Graph: the replays are timed; the dominant kernel's launch times come from an
     # eager pass of the same steps right after (events cannot be timed inside a replay)
     live = EventTracer(keys={dom})
+    sync = getattr(tr.unet._rdn_flat, "grad_sync", None) if world > 1 else None
     if graph:
         el, loss = tr.timed(args.steps, world, None)
+        if sync is not None:
+            sync.timing = []   # (events only in the eager pass: a replay cannot be timed inside)
         el_eager, _ = tr.timed(args.steps, world, live)
     else:
+        if sync is not None:
+            sync.timing = []
         el, loss = tr.timed(args.steps, world, live)
         el_eager = el
+    exposed = None
+    if sync is not None:
+        mine = sync.exposed_ms()
+        sync.timing = None
+        ex = torch.zeros(world, dtype=torch.float64)
+        ex[rank] = -1.0 if mine is None else mine
+        dist.all_reduce(ex, group=cpu_group)   # (each rank fills its own slot)
+        per = [None if v < 0 else round(v, 4) for v in ex.tolist()]
+        vals = [v for v in per if v is not None]
+        exposed = {"per_rank": per, "max": max(vals) if vals else None,
+                   "mean": round(sum(vals) / len(vals), 4) if vals else None, "unit": "ms per step",
+                   "note": "eager pass of the timed steps: end of the last gradient bucket's all-reduce on the "
+                           "comm stream minus the end of the backward on the compute stream (0 when hidden)"}
     if world > 1:
         tt = torch.tensor([el, el_eager], device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -745,6 +848,7 @@ def main():
             "fp32_images_per_s": extra["fp32"]["images_per_s"] if extra else None,
             "extra_configs": extra,
             "roofline": roof,
+            "exposed_allreduce_ms": exposed,
             "peak_hbm_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 2),
             "cpu_baseline": cpu,
             "inference": infer,

@@ -5,6 +5,7 @@ import json
 import os
 import subprocess
 import sys
+import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -70,3 +71,26 @@ def test_graph_capture_failure_restarts_eagerly():
     assert sorted(d["rank"] for d in ranks) == [0, 1]
     assert all(d["graph"] == "off" for d in ranks)
     assert "running the job again eagerly" in r.stderr
+
+
+def test_deadline_kills_a_hung_rank():
+    """Every rank hung in a collective must not hang the caller: past --deadline-s the
+    launcher kills the ranks still running and exits with EXIT_DEADLINE (124)."""
+    t0 = time.monotonic()
+    r = _bench("--gpus", "2", "--launch-dry-run", "--deadline-s", "4", env={"RDN_BENCH_DRY_HANG": "1"}, timeout=120)
+    assert r.returncode == 124, (r.returncode, r.stderr)
+    assert time.monotonic() - t0 < 60
+    assert "deadline of 4 s passed with rank(s) [1]" in r.stderr
+    assert [d["rank"] for d in _lines(r.stdout)] == [0]   # (rank 0 finished normally)
+
+
+def test_watchdog_ends_a_hung_rank_under_an_external_launcher():
+    """Under torchrun the bench's launcher is not there: the rank's own watchdog
+    thread ends the process with 124 at the deadline."""
+    t0 = time.monotonic()
+    r = _bench("--gpus", "2", "--launch-dry-run", "--deadline-s", "3",
+               env={"WORLD_SIZE": "2", "RANK": "1", "LOCAL_RANK": "1", "MASTER_ADDR": "127.0.0.1",
+                    "MASTER_PORT": "29556", "RDN_BENCH_DRY_HANG": "1"}, timeout=120)
+    assert r.returncode == 124, (r.returncode, r.stderr)
+    assert time.monotonic() - t0 < 60
+    assert "deadline of 3 s passed" in r.stderr

@@ -114,3 +114,34 @@ def test_gradsync_world2_gloo_average(tmp_path, defer, bucket_mb, tail_mb):
     avg = (res[0][0] + res[1][0]) / 2
     torch.testing.assert_close(res[0][1], avg)
     torch.testing.assert_close(res[1][1], avg)
+
+
+def test_capture_drain_refuses_unsafe_nccl_groups(monkeypatch):
+    """train_graph._drain_collectives (before capturing an RCCL train step): a torch
+    build without ProcessGroupNCCL._wait_for_pending_works, or an NCCL group set up
+    without TORCH_NCCL_CUDA_EVENT_CACHE=0, raises GraphCaptureUnsafe instead of
+    capturing into a possible watchdog abort (bench.py turns it into the eager path)."""
+    import torch.distributed as dist
+    from vub_image_denoising_amd import train_graph as TG
+
+    class PG:   # an NCCL group of a torch build without the private drain method
+        pass
+
+    class PGDrain:
+        drained = 0
+
+        def _wait_for_pending_works(self):
+            PGDrain.drained += 1
+
+    monkeypatch.setattr(dist, "is_initialized", lambda: True)
+    monkeypatch.setattr(dist, "get_backend", lambda pg=None: "nccl")
+    monkeypatch.setenv("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
+    monkeypatch.setattr(type(dist.group), "WORLD", property(lambda cls: PG()), raising=False)
+    with pytest.raises(TG.GraphCaptureUnsafe, match="_wait_for_pending_works"):
+        TG._drain_collectives(None)
+    monkeypatch.setattr(type(dist.group), "WORLD", property(lambda cls: PGDrain()), raising=False)
+    TG._drain_collectives(None)
+    assert PGDrain.drained == 1
+    monkeypatch.setenv("TORCH_NCCL_CUDA_EVENT_CACHE", "1")
+    with pytest.raises(TG.GraphCaptureUnsafe, match="TORCH_NCCL_CUDA_EVENT_CACHE"):
+        TG._drain_collectives(None)

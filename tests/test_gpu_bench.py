@@ -38,3 +38,7 @@ def test_bench_launcher_two_ranks_gloo():
     assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 4
     assert d["config"]["launcher"] == "bench.py child processes" and d["config"]["dist_backend"] == "gloo"
     assert d["value"] > 0 and d["cpu_baseline"] is None
+    # the all-reduce time the backward did not hide, per rank (eager pass of the timed steps)
+    ex = d["exposed_allreduce_ms"]
+    assert len(ex["per_rank"]) == 2 and all(v is not None and v >= 0 for v in ex["per_rank"]), ex
+    assert ex["max"] == max(ex["per_rank"])

@@ -95,3 +95,52 @@ def test_ddp_two_ranks_match_single_process(tmp_path, case):
 def _param_ranges(model):
     fp = model.unet._rdn_flat
     return [(o, o + p.numel()) for p, o in zip(fp.params, fp.offsets)]
+
+
+def _rank_accum(rank, world, init_file, q):
+    try:
+        dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
+        from vub_image_denoising_amd.ddp import GradSync
+        from vub_image_denoising_amd.diffusion_RDUnet import train_step_device
+        model, clean, noisy, t = _setup("fp32", 16, 32)
+        opt = torch.optim.SGD(model.parameters(), lr=0.0)
+        sl = slice(2 * rank, 2 * rank + 2)
+        train_step_device(model, clean[sl], noisy[sl], opt, clip_value=1.0, t=t[sl])  # builds the flat buffer
+        model.unet._rdn_flat.grad_sync = GradSync(model.unet._rdn_flat, bucket_mb=0.5)
+        train_step_device(model, clean[sl], noisy[sl], opt, clip_value=1.0, t=t[sl], clip=False)
+        train_step_device(model, clean[sl], noisy[sl], opt, clip_value=1.0, t=t.flip(0)[sl], zero_grad=False)
+        torch.cuda.synchronize()
+        q.put((rank, torch.cat([p.grad.flatten() for p in model.parameters()]).cpu().numpy()))
+        dist.destroy_process_group()
+    except Exception as e:  # report instead of hanging the parent on q.get
+        q.put((rank, repr(e)))
+
+
+def test_ddp_accumulate_then_clip(tmp_path):
+    """zero_grad=False with clip=True (advisor r04): the gradients held from the
+    previous call are already averaged, so the 1/world factor must not be folded
+    into this clip -- two ranks equal one process accumulating the same two
+    half-batch-per-rank steps, then clipping."""
+    from vub_image_denoising_amd.diffusion_RDUnet import train_step_device
+    model, clean, noisy, t = _setup("fp32", 16, 32)
+    opt = torch.optim.SGD(model.parameters(), lr=0.0)
+    train_step_device(model, clean, noisy, opt, clip_value=1.0, t=t, clip=False)
+    train_step_device(model, clean, noisy, opt, clip_value=1.0, t=t.flip(0), zero_grad=False)
+    torch.cuda.synchronize()
+    ref = torch.cat([p.grad.flatten() for p in model.parameters()]).cpu().numpy()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank_accum, args=(r, 2, str(tmp_path / "rdv"), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        r, g = q.get(timeout=110)
+        assert not isinstance(g, str), g
+        res[r] = g
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    assert np.array_equal(res[0], res[1])
+    err = np.linalg.norm(res[0] - ref) / np.linalg.norm(ref)
+    assert err < 1e-5, err

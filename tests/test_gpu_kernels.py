@@ -422,13 +422,16 @@ def test_fused_prelu_gate_matches_separate_pass(dt):
     (96, 32, 96, False, False),   # up_0.conv (CK=96, one block per CU)
     (8, 32, 8, False, False),     # input conv
 ])
-def test_conv3_ws_matches_halo(cin, cout, Cs_in, gate, accum):
+@pytest.mark.parametrize("full", [False, True])
+def test_conv3_ws_matches_halo(cin, cout, Cs_in, gate, accum, full):
     """The weight-stationary persistent kernel (default for bf16 single-chunk,
     <= 96-column layers) against the K-streaming halo kernel (forced with an
     explicit bn) on a multi-tile ragged image: every tile, flag and the gate
-    must give bitwise-identical results (same MFMA k order, same epilogue)."""
+    must give bitwise-identical results (same MFMA k order, same epilogue).
+    full: whole 8 x 16 tiles, where conv3_ws runs its accumulator epilogue
+    (round 5: swapped MFMA operands, stores from the registers)."""
     dt, code, lib, st = torch.bfloat16, H.RDN_BF16, H.lib(), H.stream_ptr()
-    N, Hh, Ww = 6, 120, 136          # 810 tiles: several tiles per persistent block
+    N, Hh, Ww = (4, 64, 128) if full else (6, 120, 136)   # 256 / 810 tiles: several per persistent block
     P = N * Hh * Ww
     x = torch.randn(P, Cs_in, device="cuda").to(dt)
     w = (torch.randn(cout, cin, 3, 3, device="cuda") / (3 * cin ** 0.5)).contiguous()
@@ -451,6 +454,11 @@ def test_conv3_ws_matches_halo(cin, cout, Cs_in, gate, accum):
                        bn=bn)
         if gate:
             d.gate, d.gate_ps, d.gate_alpha = pre_in.data_ptr(), cin, ga.data_ptr()
+        if bn == 0:
+            name = C.create_string_buffer(128)
+            H.check(lib.rdn_conv_kernel_name(C.byref(d), name, 128))
+            if name.value.decode().startswith("conv3_ws_kernel"):   # (else conv3_wsd: full 96-channel tiles)
+                assert name.value.decode().endswith(",ae>") == full, name.value
         H.check(lib.rdn_conv_fwd(C.byref(d), st))
         outs.append((out, pre))
     torch.cuda.synchronize()

@@ -34,6 +34,9 @@ using c3::TH;
 using c3::TW;
 
 constexpr int LDS_2BLK = 80 * 1024;     // two resident blocks per CU below this
+#ifndef WS_PF
+#define WS_PF 0   // accumulator-epilogue path: k-steps of fragments read ahead of the MFMAs
+#endif
 constexpr int LDS_MAX = 160 * 1024;
 
 template <int BN, int CK>
@@ -64,7 +67,14 @@ struct WsCfg {
   static constexpr int BLK_PER_CU = LDS <= LDS_2BLK ? 2 : 1;
 };
 
-template <int BN, int CK, bool GATE>
+// AE (round 5, "accumulator epilogue"): full 8 x 16 tiles with NHWC outputs only.  The
+// MFMAs run with swapped operands (A = weight rows, B = halo pixels), so a lane's
+// accumulators are 4 consecutive output channels of one pixel, and the epilogue
+// (bias, PReLU-input store, PReLU, residual / accumulate operand prefetched a tile
+// ahead, output) goes from the accumulators straight to 8-byte stores, as in
+// conv3_dense / conv3_dw: no fp32 tile through LDS and two barriers fewer per tile.
+// The sums are the same MFMA k-sequence over the same operands (bit-identical).
+template <int BN, int CK, bool GATE, bool AE>
 __global__ __launch_bounds__(NT, 2) void conv3_ws_kernel(rdn_conv_desc d, int tiles_x, int tiles_y, int ntiles) {
   using Cfg = WsCfg<BN, CK>;
   constexpr int VEC = 8;
@@ -224,8 +234,14 @@ __global__ __launch_bounds__(NT, 2) void conv3_ws_kernel(rdn_conv_desc d, int ti
       const int hy = hp / (TW + 2), hx = hp - hy * (TW + 2);
       const bool ok = ((it + 1 < H_IT) || u < H_UNITS) & ((unsigned)(oy - 1 + hy) < (unsigned)H) &
                       ((unsigned)(ox - 1 + hx) < (unsigned)W);
+#ifdef WS_DIAG_NO_LOAD   // diagnostic build: no halo loads (operands stay finite)
+      (void)rx; (void)rg;
+      hreg[it] = u32x4{(unsigned)ok, 0u, 0u, 0u};
+      if constexpr (GATE) greg[it] = u32x4{0u, 0u, 0u, 0u};
+#else
       hreg[it] = rdn_ld16(rx, ok, hrel[it] * 2);
       if constexpr (GATE) greg[it] = rdn_ld16(rg, ok, grel[it] * 2);
+#endif
     }
   };
   auto store_halo = [&](const u32x4 (&hreg)[H_IT], const u32x4 (&greg)[GH]) {
@@ -265,6 +281,116 @@ __global__ __launch_bounds__(NT, 2) void conv3_ws_kernel(rdn_conv_desc d, int ti
       const bool ok = full && ((it + 1 < E_IT) || tid + it * NT < EU) && c < (pf_res ? d.res_climit : d.ncols);
       eop[it] = rdn_ld16(rb, ok, (erel[it] * ps + (pf_res ? off_res(c) : off_out(c))) * 2);
     }
+  };
+
+  // ---- AE: per-lane channel offsets / bias / slope of its (n-tile, 4-channel group)s
+  const bool ae_res = flags & RDN_EPI_RESID, ae_acc = flags & RDN_EPI_ACCUM;
+  int ae_co[AE ? NTL : 1], ae_cp[AE ? NTL : 1], ae_ce[AE ? NTL : 1];
+  bool ae_eok[AE ? NTL : 1];
+  f32x4 ae_b[AE ? NTL : 1], ae_a[AE ? NTL : 1];
+  if constexpr (AE) {
+#pragma unroll
+    for (int jn = 0; jn < NTL; ++jn) {
+      const int c = jn * 16 + 4 * g;
+      const bool in = c < d.ncols;
+      ae_co[jn] = rdn_coff32(d.out_c0 + c, (int)d.out_ps, (int)d.out_pl);
+      ae_cp[jn] = rdn_coff32(c, (int)d.pre_ps, (int)d.pre_pl);
+      ae_eok[jn] = in && (ae_res ? c < d.res_climit : ae_acc);
+      ae_ce[jn] = ae_res ? rdn_coff32(d.res_c0 + c, (int)d.res_ps, (int)d.res_pl) : ae_co[jn];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        ae_b[jn][e] = ((flags & RDN_EPI_BIAS) && in) ? d.bias[c + e] : 0.f;
+        ae_a[jn][e] = ((flags & RDN_EPI_PRELU) && in) ? d.alpha[c + e] : 0.f;
+      }
+    }
+  }
+  // (AE) residual / accumulate operand of a tile: lane (r, g) reads its 4 channels of
+  // pixel (tile row 2 wave + i, column r)
+  auto ae_load = [&](int oy, int ox, int on, u32x2 (&ae_eo)[MT][NTL]) {
+    if constexpr (AE) {
+      const int64_t opix0 = ((int64_t)on * H + oy) * W + ox;
+      const int eps = ae_res ? (int)d.res_ps : (int)d.out_ps;
+      const __amdgpu_buffer_rsrc_t rb =
+          rdn_rsrc(ae_res ? (const bf16*)d.res + opix0 * d.res_ps : (const bf16*)d.out + opix0 * d.out_ps);
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int jn = 0; jn < NTL; ++jn)
+          ae_eo[i][jn] = rdn_ld8(rb, ae_eok[jn], (((2 * wave + i) * W + r) * eps + ae_ce[jn]) * 2);
+    }
+  };
+  auto ae_tile = [&](int y0, int x0, int nimg, const u32x2 (&ae_eo)[MT][NTL]) {
+    f32x4 acc[MT][NTL];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int jn = 0; jn < NTL; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // fragments of k-step j + WS_PF read before the MFMAs of j (a sched barrier keeps
+    // them there: hipcc's own schedule waited on each read one MFMA pair later)
+    constexpr int PF = WS_PF, NB = PF + 1;
+    u32x4 af[NB][MT], bfr[NB][NTL];
+    auto rd = [&](int j, int b) {
+      int ao;
+      if constexpr (KALIGN) {
+        const int k0 = 32 * j;
+        int tap = k0 / CK;
+        const int ci = k0 - tap * CK;
+        tap = tap < 9 ? tap : 8;
+        ao = ((tap / 3) * (TW + 2) + tap % 3) * HROW + ci * 2;
+      } else {
+        ao = offA[j];
+      }
+#pragma unroll
+      for (int i = 0; i < MT; ++i) af[b][i] = *(const u32x4*)(pa + ao + i * (TW + 2) * HROW);
+#pragma unroll
+      for (int jn = 0; jn < NTL; ++jn) bfr[b][jn] = *(const u32x4*)(pb + jn * 16 * WROW + j * 64);
+    };
+#pragma unroll
+    for (int p = 0; p < PF && p < NSTEP; ++p) rd(p, p);
+#pragma unroll
+    for (int j = 0; j < NSTEP; ++j) {
+      if (j + PF < NSTEP) rd(j + PF, (j + PF) % NB);
+      if constexpr (PF > 0) __builtin_amdgcn_sched_barrier(0);
+      if constexpr (PF == 0) rd(j, 0);
+      const int b = j % NB;
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int jn = 0; jn < NTL; ++jn)   // D^T[m = column][n = pixel]
+#ifdef WS_DIAG_NO_MFMA   // diagnostic build: fragments consumed without MFMAs
+          acc[i][jn][0] += __builtin_bit_cast(float, bfr[b][jn][0] ^ af[b][i][0]);
+#else
+          acc[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bfr[b][jn]),
+                                                               __builtin_bit_cast(bf16x8, af[b][i]), acc[i][jn], 0,
+                                                               0, 0);
+#endif
+    }
+    const int64_t opix0 = ((int64_t)nimg * H + y0) * W + x0;
+    bf16* const ob = (bf16*)d.out + opix0 * d.out_ps;
+    bf16* const pb_ = (bf16*)d.pre + opix0 * d.pre_ps;
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int jn = 0; jn < NTL; ++jn) {
+        if (jn * 16 + 4 * g >= d.ncols) continue;
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc[i][jn][e] + ae_b[jn][e];
+        const int prow = (2 * wave + i) * W + r;
+        if (flags & RDN_EPI_STORE_PRE) *(u32x2*)(pb_ + prow * (int)d.pre_ps + ae_cp[jn]) = rdn_pack4(v);
+        if (flags & RDN_EPI_PRELU) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = v[e] > 0.f ? v[e] : ae_a[jn][e] * v[e];
+        }
+        if (ae_eok[jn]) {
+          v[0] += bf16lo(ae_eo[i][jn][0]); v[1] += bf16hi(ae_eo[i][jn][0]);
+          v[2] += bf16lo(ae_eo[i][jn][1]); v[3] += bf16hi(ae_eo[i][jn][1]);
+        }
+#ifdef WS_DIAG_NO_STORE   // diagnostic build: no output stores (values stay live)
+        if (flags & (1 << 30))
+#endif
+        *(u32x2*)(ob + prow * (int)d.out_ps + ae_co[jn]) = rdn_pack4(v);
+      }
   };
 
   // the tile whose halo is in LDS: 9 taps x MFMA, then the fused epilogue
@@ -373,6 +499,35 @@ __global__ __launch_bounds__(NT, 2) void conv3_ws_kernel(rdn_conv_desc d, int ti
   const int t_last = t_hi - 1;
   int y0, x0, nimg;
   origin(t, y0, x0, nimg);
+  if constexpr (AE) {
+    // step: issue the next tile's halo and epilogue operand, this tile's MFMAs and its
+    // epilogue from the accumulators, one barrier (halo consumed), the next halo to
+    // LDS, one barrier (visible)
+    u32x2 eC[MT][NTL], eN[MT][NTL];
+    load_halo(y0, x0, nimg, hA, gA);
+    store_halo(hA, gA);
+    ae_load(y0, x0, nimg, eC);
+    __syncthreads();
+    int t1 = t + per;
+    for (;;) {
+      int y1 = 0, x1 = 0, n1 = 0;
+      origin(min(t1, t_last), y1, x1, n1);
+      load_halo(y1, x1, n1, hA, gA);
+      ae_load(y1, x1, n1, eN);
+      ae_tile(y0, x0, nimg, eC);
+      if (t1 >= t_hi) break;
+      __syncthreads();   // this tile's halo consumed by every wave
+      store_halo(hA, gA);
+      __syncthreads();   // next halo visible
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int jn = 0; jn < NTL; ++jn) eC[i][jn] = eN[i][jn];
+      y0 = y1; x0 = x1; nimg = n1;
+      t1 += per;
+    }
+    return;
+  }
   load_halo(y0, x0, nimg, hA, gA);
   load_epi(y0, x0, nimg);
   store_halo(hA, gA);
@@ -403,6 +558,15 @@ int ws_enabled() {
   return on;
 }
 
+// the accumulator epilogue where it applies (RDN_WS_AE=0: the LDS-tile epilogue, for A/B)
+bool ws_ae_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("RDN_WS_AE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // resident blocks per CU of one instantiation (registers, LDS, waves), from the
 // runtime's occupancy calculator, capped at 4; the persistent grid is sized to it
 template <typename K>
@@ -412,9 +576,9 @@ int resident_per_cu(K kernel, int cap) {
   return n < cap ? n : cap;
 }
 
-template <int BN, int CK, bool GATE>
+template <int BN, int CK, bool GATE, bool AE>
 int launch_ws_k(const rdn_conv_desc* d, hipStream_t st, int tiles_x, int tiles_y, int ntiles, int cus) {
-  auto kern = conv3_ws_kernel<BN, CK, GATE>;
+  auto kern = conv3_ws_kernel<BN, CK, GATE, AE>;
   static const int bpc = resident_per_cu(kern, 4);   // persistent blocks per CU: what is resident
   const int per_xcd = (ntiles + 7) / 8;
   int slots = cus * bpc / 8;
@@ -454,15 +618,29 @@ int launch_ws(const rdn_conv_desc* d, hipStream_t st) {
     cus = cached_cus;
     constexpr int HU = CK / 8;
     if (d->gate && NT % HU != 0) return 1;
-    RDN_PROBE("conv3_ws_kernel<bf16,%d,%d%s>", BN, CK, d->gate ? ",gate" : "");
+    // accumulator epilogue: full tiles, NHWC 4-channel groups, 8-byte aligned operands
+    const int64_t span = (int64_t)TH * d->w;
+    auto ok4 = [](int64_t ps, int64_t c0, const void* p) { return ps % 4 == 0 && c0 % 4 == 0 && !((uintptr_t)p & 7); };
+    auto fit = [&](int64_t ps, int64_t pl, int c_hi) {
+      return 2 * (span * ps + rdn_coff(c_hi, ps, pl)) < (int64_t)RDN_OOB - 16;
+    };
+    const bool ae = ws_ae_enabled() && d->h % TH == 0 && d->w % TW == 0 && d->ncols % 4 == 0 &&
+                    !(d->flags & RDN_EPI_OUT_NCHW) && ok4(d->out_ps, d->out_c0, d->out) &&
+                    fit(d->out_ps, d->out_pl, d->out_c0 + d->ncols) &&
+                    (!(d->flags & RDN_EPI_STORE_PRE) || (ok4(d->pre_ps, 0, d->pre) && fit(d->pre_ps, d->pre_pl, d->ncols))) &&
+                    (!(d->flags & RDN_EPI_RESID) ||
+                     (ok4(d->res_ps, d->res_c0, d->res) && d->res_climit % 4 == 0 && fit(d->res_ps, d->res_pl, d->res_c0 + d->ncols)));
+    RDN_PROBE("conv3_ws_kernel<bf16,%d,%d%s%s>", BN, CK, d->gate ? ",gate" : "", ae ? ",ae" : "");
     if (d->gate) {
       if constexpr (NT % HU == 0) {
-        return launch_ws_k<BN, CK, true>(d, st, tiles_x, tiles_y, ntiles, cus);
+        return ae ? launch_ws_k<BN, CK, true, true>(d, st, tiles_x, tiles_y, ntiles, cus)
+                  : launch_ws_k<BN, CK, true, false>(d, st, tiles_x, tiles_y, ntiles, cus);
       } else {
         return 1;
       }
     }
-    return launch_ws_k<BN, CK, false>(d, st, tiles_x, tiles_y, ntiles, cus);
+    return ae ? launch_ws_k<BN, CK, false, true>(d, st, tiles_x, tiles_y, ntiles, cus)
+              : launch_ws_k<BN, CK, false, false>(d, st, tiles_x, tiles_y, ntiles, cus);
   }
 }
 

@@ -114,6 +114,10 @@ class GradSync:
         # `pending` for the caller's clip (take_pending) instead of scaling
         self.defer_average = False
         self.pending = None
+        # set to a list to time each finish(): (backward done on the compute stream,
+        # last bucket's all-reduce done on the comm stream) event pairs -- the
+        # all-reduce time the backward did not hide (bench.py exposed_allreduce_ms)
+        self.timing = None
 
     # --- engine hooks -------------------------------------------------
     def begin(self, buf=None):
@@ -163,10 +167,18 @@ class GradSync:
 
     def finish(self):
         """Launch what is left (in bucket order), wait, and average."""
+        e0 = None
+        if self.timing is not None and self.overlap:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record(torch.cuda.current_stream())   # the backward's last kernel is behind this
         for b in range(len(self.buckets)):
             if not self._launched[b] and self.overlap:
                 self._srcs[b].append(torch.cuda.current_stream())
             self._launch(b)
+        if e0 is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record(self.stream)                    # behind the last bucket's all-reduce
+            self.timing.append((e0, e1))
         for w in self._works:
             w.wait()
         if self.overlap:
@@ -177,6 +189,15 @@ class GradSync:
                 self.pending = 1.0 / self.world
             else:
                 self._average()
+
+    def exposed_ms(self):
+        """Mean over the timed finish() calls of max(0, comm end - backward end), ms
+        (synchronises the device); None if nothing was timed."""
+        if not self.timing:
+            return None
+        torch.cuda.synchronize()
+        xs = [max(0.0, a.elapsed_time(b)) for a, b in self.timing]
+        return sum(xs) / len(xs)
 
     def take_pending(self):
         """The 1/world factor a deferred finish() left unapplied (None if none);

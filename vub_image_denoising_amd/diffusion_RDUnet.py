@@ -105,9 +105,11 @@ def train_step_device(model, clean_images, noisy_images, optimizer, distribution
     loss = _forward_loss(model, clean_images, noisy_images, distribution_choice, t)
     # data-parallel: the clip right after the backward also applies the 1/world
     # average of the all-reduced gradient (one pass instead of two, ddp.py)
+    # -- only when the gradients are this backward's alone (zero_grad): accumulated
+    # ones already hold averaged sums from earlier calls, which must not be scaled again
     fp = getattr(model.unet, "_rdn_flat", None)
     sync = getattr(fp, "grad_sync", None) if clip else None
-    fold = sync is not None and sync.world > 1
+    fold = sync is not None and sync.world > 1 and zero_grad
     if fold:
         sync.defer_average = True
     try:

@@ -245,6 +245,36 @@ def _mixed(make, patch_size):
     return (None if tr[0] is None else MixedPatchLoader(tr)), MixedPatchLoader(va)
 
 
+def _cell_split(pools, n_levels, dataset_percentage, validation_split, generator):
+    """Train / validation split of several patch grids over the SAME images (config
+    5's mixed sizes): the unit is a cell of the largest grid -- (image, top // P,
+    left // P), P the largest patch size; every patch lies in exactly one cell, since
+    the grids all start at 0 with strides dividing P -- and a cell goes wholly to one
+    side, with all its patches of every size and every noise level.  So no validation
+    patch of one size shares a pixel with a training patch of another (the per-size
+    index splits of round 4 let ~80 % of the 128-pixel validation patches lie inside
+    256-pixel training patches).  The cells themselves are split as data_loader.py:
+    63-74 splits items (optional random subset, then random_split).  Returns one
+    (train, val) index-list pair per pool (index = patch * n_levels + level)."""
+    P = max(pl.patch_size for pl in pools)
+    if any(P % pl.patch_size for pl in pools):
+        raise ValueError("mixed patch sizes must divide the largest one")
+    cell_of = [[(k, top // P, left // P) for k, top, left in pl.patches] for pl in pools]
+    cells = sorted({c for cs in cell_of for c in cs})
+    tr_c, va_c = _split(len(cells), dataset_percentage, validation_split, generator)
+    side = {cells[i]: 0 for i in tr_c}
+    side.update({cells[i]: 1 for i in va_c})
+    out = []
+    for cs in cell_of:
+        tr, va = [], []
+        for j, c in enumerate(cs):
+            s_ = side.get(c)
+            if s_ is not None:
+                (tr if s_ == 0 else va).extend(j * n_levels + lv for lv in range(n_levels))
+        out.append((tr, va))
+    return out
+
+
 def _split(total, dataset_percentage, validation_split, generator):
     """data_loader.py:63-74: optional random subset, then the train/val random_split."""
     idx = list(range(total))
@@ -269,6 +299,17 @@ def load_data_gpu(image_folder, batch_size=4, validation_split=0.2, augment=Fals
             exts = ("png", "jpg", "jpeg")
             images = [_read_image(os.path.join(image_folder, f), use_rgb) for f in sorted(os.listdir(image_folder))
                       if f.lower().endswith(exts)]
+        sizes = _sizes(patch_size)
+        if len(sizes) > 1 and not only_validation:   # one split over cells of the largest grid
+            pools = [PatchPool(images, ps, device) for ps in sizes]
+            levels = train_noise_levels if train_noise_levels is not None else [15, 25, 50]
+            g = torch.Generator().manual_seed(seed)
+            splits = _cell_split(pools, len(levels), dataset_percentage, validation_split, g)
+            tr = [GpuLoader(pl, a, batch_size, levels, True, augment, seed + 1, include_noise_level)
+                  for pl, (a, _) in zip(pools, splits)]
+            va = [GpuLoader(pl, b, batch_size, levels, False, augment, seed + 2, include_noise_level)
+                  for pl, (_, b) in zip(pools, splits)]
+            return MixedPatchLoader(tr), MixedPatchLoader(va)
         return _mixed(lambda ps: load_data_gpu(image_folder, batch_size, validation_split, augment, dataset_percentage,
                                                only_validation, include_noise_level, train_noise_levels,
                                                val_noise_levels, use_rgb, ps, seed, device,
@@ -295,6 +336,15 @@ def load_sidd_data_gpu(root_folder, batch_size=4, validation_split=0.2, augment=
         pairs = sidd_pairs(root_folder)
         gts = [_read_image(g, use_rgb) for _, g in pairs]
         noisy = [_read_image(n, use_rgb) for n, _ in pairs]
+        sizes = _sizes(patch_size)
+        if len(sizes) > 1 and not only_validation:   # one split over cells of the largest grid
+            pools = [PatchPool(gts, ps, device, noisy_images=noisy) for ps in sizes]
+            g = torch.Generator().manual_seed(seed)
+            splits = _cell_split(pools, 1, dataset_percentage, validation_split, g)
+            return (MixedPatchLoader([GpuLoader(pl, a, batch_size, None, True, augment, seed + 1)
+                                      for pl, (a, _) in zip(pools, splits)]),
+                    MixedPatchLoader([GpuLoader(pl, b, batch_size, None, False, augment, seed + 2)
+                                      for pl, (_, b) in zip(pools, splits)]))
         return _mixed(lambda ps: load_sidd_data_gpu(root_folder, batch_size, validation_split, augment,
                                                     dataset_percentage, only_validation, use_rgb, ps, seed, device,
                                                     pool=PatchPool(gts, ps, device, noisy_images=noisy)),

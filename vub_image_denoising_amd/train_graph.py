@@ -26,11 +26,17 @@ backward writes); an eager step in between is allowed and does not disturb it.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .diffusion_RDUnet import sample_biased, train_step_device
 from .engine import find_flat
 from .optim import FusedAdam
+
+
+class GraphCaptureUnsafe(RuntimeError):
+    """Capturing the data-parallel step is not safe on this torch build."""
 
 
 def _drain_collectives(fp) -> None:
@@ -51,7 +57,17 @@ def _drain_collectives(fp) -> None:
                 continue
         except (RuntimeError, ValueError):
             continue
-        pg._wait_for_pending_works()
+        if os.environ.get("TORCH_NCCL_CUDA_EVENT_CACHE") != "0":
+            # with the event cache on, an eager collective's cached event can be re-recorded
+            # inside the capture and the watchdog's query of it aborts the process (ddp.capture_safe_env)
+            raise GraphCaptureUnsafe("capturing an RCCL train step needs TORCH_NCCL_CUDA_EVENT_CACHE=0 set before "
+                                     "init_process_group (call ddp.capture_safe_env() first)")
+        wait = getattr(pg, "_wait_for_pending_works", None)
+        if wait is None:   # (a private ProcessGroupNCCL method; a build without it cannot capture safely)
+            raise GraphCaptureUnsafe(
+                "torch.distributed's NCCL process group has no _wait_for_pending_works(): the watchdog may query "
+                "a captured event and abort the process, so the RCCL train step is not captured (run eagerly)")
+        wait()
 
 
 def _node_count(g):
