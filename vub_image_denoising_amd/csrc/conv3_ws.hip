@@ -34,6 +34,9 @@ using c3::TH;
 using c3::TW;
 
 constexpr int LDS_2BLK = 80 * 1024;     // two resident blocks per CU below this
+#ifndef WS_W16
+#define WS_W16 1  // accumulator epilogue in 16-byte units (pixel-row pairs swapped between lane rows)
+#endif
 #ifndef WS_PF
 #define WS_PF 0   // accumulator-epilogue path: k-steps of fragments read ahead of the MFMAs
 #endif
@@ -288,10 +291,14 @@ __global__ __launch_bounds__(NT, 2) void conv3_ws_kernel(rdn_conv_desc d, int ti
   int ae_co[AE ? NTL : 1], ae_cp[AE ? NTL : 1], ae_ce[AE ? NTL : 1];
   bool ae_eok[AE ? NTL : 1];
   f32x4 ae_b[AE ? NTL : 1], ae_a[AE ? NTL : 1];
+  f32x4 ae_b2[AE && WS_W16 && BN <= 64 ? NTL : 1], ae_a2[AE && WS_W16 && BN <= 64 ? NTL : 1];
+  // (MT == 2: the two pixel rows of a wave pair up; up to 64 columns: the wider
+  // instantiations spilled with the second bias / slope registers)
+  constexpr bool W16 = AE && WS_W16 && BN <= 64;
   if constexpr (AE) {
 #pragma unroll
     for (int jn = 0; jn < NTL; ++jn) {
-      const int c = jn * 16 + 4 * g;
+      const int c = jn * 16 + (W16 ? 8 * (g >> 1) : 4 * g);
       const bool in = c < d.ncols;
       ae_co[jn] = rdn_coff32(d.out_c0 + c, (int)d.out_ps, (int)d.out_pl);
       ae_cp[jn] = rdn_coff32(c, (int)d.pre_ps, (int)d.pre_pl);
@@ -301,6 +308,10 @@ __global__ __launch_bounds__(NT, 2) void conv3_ws_kernel(rdn_conv_desc d, int ti
       for (int e = 0; e < 4; ++e) {
         ae_b[jn][e] = ((flags & RDN_EPI_BIAS) && in) ? d.bias[c + e] : 0.f;
         ae_a[jn][e] = ((flags & RDN_EPI_PRELU) && in) ? d.alpha[c + e] : 0.f;
+        if constexpr (W16) {   // (the unit's second half: channels c + 4 ..)
+          ae_b2[jn][e] = ((flags & RDN_EPI_BIAS) && in) ? d.bias[c + 4 + e] : 0.f;
+          ae_a2[jn][e] = ((flags & RDN_EPI_PRELU) && in) ? d.alpha[c + 4 + e] : 0.f;
+        }
       }
     }
   }
@@ -312,6 +323,15 @@ __global__ __launch_bounds__(NT, 2) void conv3_ws_kernel(rdn_conv_desc d, int ti
       const int eps = ae_res ? (int)d.res_ps : (int)d.out_ps;
       const __amdgpu_buffer_rsrc_t rb =
           rdn_rsrc(ae_res ? (const bf16*)d.res + opix0 * d.res_ps : (const bf16*)d.out + opix0 * d.out_ps);
+      if constexpr (W16) {   // one 16-byte unit per n-tile: [0][jn] its low, [1][jn] its high half
+#pragma unroll
+        for (int jn = 0; jn < NTL; ++jn) {
+          const u32x4 q = rdn_ld16(rb, ae_eok[jn], (((2 * wave + (g & 1)) * W + r) * eps + ae_ce[jn]) * 2);
+          ae_eo[0][jn] = u32x2{q[0], q[1]};
+          ae_eo[1][jn] = u32x2{q[2], q[3]};
+        }
+        return;
+      }
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -368,6 +388,49 @@ __global__ __launch_bounds__(NT, 2) void conv3_ws_kernel(rdn_conv_desc d, int ti
     const int64_t opix0 = ((int64_t)nimg * H + y0) * W + x0;
     bf16* const ob = (bf16*)d.out + opix0 * d.out_ps;
     bf16* const pb_ = (bf16*)d.pre + opix0 * d.pre_ps;
+    if constexpr (W16) {
+      static_assert(MT == 2, "W16 pairs the two pixel rows of a wave");
+#pragma unroll
+      for (int jn = 0; jn < NTL; ++jn) {
+        if (jn * 16 + 8 * (g >> 1) >= d.ncols) continue;
+        // (whole-vector bit casts only: rdn_common.h's note on ext_vector elements)
+        const u32x4 ua = __builtin_bit_cast(u32x4, acc[0][jn]), ub = __builtin_bit_cast(u32x4, acc[1][jn]);
+        u32x4 lo, hi;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const auto sw = __builtin_amdgcn_permlane16_swap(ua[e], ub[e], false, false);
+          lo[e] = sw[0];
+          hi[e] = sw[1];
+        }
+        const f32x4 flo = __builtin_bit_cast(f32x4, lo), fhi = __builtin_bit_cast(f32x4, hi);
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] = flo[e] + ae_b[jn][e];
+          v[4 + e] = fhi[e] + ae_b2[jn][e];
+        }
+        const int prow = (2 * wave + (g & 1)) * W + r;
+        if (flags & RDN_EPI_STORE_PRE) *(u32x4*)(pb_ + prow * (int)d.pre_ps + ae_cp[jn]) = Unit16<bf16>::pack(v);
+        if (flags & RDN_EPI_PRELU) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] = v[e] > 0.f ? v[e] : ae_a[jn][e] * v[e];
+            v[4 + e] = v[4 + e] > 0.f ? v[4 + e] : ae_a2[jn][e] * v[4 + e];
+          }
+        }
+        if (ae_eok[jn]) {
+          v[0] += bf16lo(ae_eo[0][jn][0]); v[1] += bf16hi(ae_eo[0][jn][0]);
+          v[2] += bf16lo(ae_eo[0][jn][1]); v[3] += bf16hi(ae_eo[0][jn][1]);
+          v[4] += bf16lo(ae_eo[1][jn][0]); v[5] += bf16hi(ae_eo[1][jn][0]);
+          v[6] += bf16lo(ae_eo[1][jn][1]); v[7] += bf16hi(ae_eo[1][jn][1]);
+        }
+#ifdef WS_DIAG_NO_STORE
+        if (flags & (1 << 30))
+#endif
+        *(u32x4*)(ob + prow * (int)d.out_ps + ae_co[jn]) = Unit16<bf16>::pack(v);
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -620,21 +683,30 @@ int launch_ws(const rdn_conv_desc* d, hipStream_t st) {
     if (d->gate && NT % HU != 0) return 1;
     // accumulator epilogue: full tiles, NHWC 4-channel groups, 8-byte aligned operands
     const int64_t span = (int64_t)TH * d->w;
-    auto ok4 = [](int64_t ps, int64_t c0, const void* p) { return ps % 4 == 0 && c0 % 4 == 0 && !((uintptr_t)p & 7); };
+    constexpr bool w16 = WS_W16 && BN <= 64;
+    auto ok4 = [](int64_t ps, int64_t c0, const void* p) {   // (w16: 16-byte units of 8 channels)
+      return w16 ? (ps % 8 == 0 && c0 % 8 == 0 && !((uintptr_t)p & 15)) : (ps % 4 == 0 && c0 % 4 == 0 && !((uintptr_t)p & 7));
+    };
     auto fit = [&](int64_t ps, int64_t pl, int c_hi) {
       return 2 * (span * ps + rdn_coff(c_hi, ps, pl)) < (int64_t)RDN_OOB - 16;
     };
-    const bool ae = ws_ae_enabled() && d->h % TH == 0 && d->w % TW == 0 && d->ncols % 4 == 0 &&
+    // (the gated 96-column accumulator-epilogue instantiation spilled: LDS-tile epilogue there)
+    const bool ae = ws_ae_enabled() && !(d->gate && BN > 80) && d->h % TH == 0 && d->w % TW == 0 && d->ncols % (w16 ? 8 : 4) == 0 &&
                     !(d->flags & RDN_EPI_OUT_NCHW) && ok4(d->out_ps, d->out_c0, d->out) &&
                     fit(d->out_ps, d->out_pl, d->out_c0 + d->ncols) &&
                     (!(d->flags & RDN_EPI_STORE_PRE) || (ok4(d->pre_ps, 0, d->pre) && fit(d->pre_ps, d->pre_pl, d->ncols))) &&
                     (!(d->flags & RDN_EPI_RESID) ||
-                     (ok4(d->res_ps, d->res_c0, d->res) && d->res_climit % 4 == 0 && fit(d->res_ps, d->res_pl, d->res_c0 + d->ncols)));
+                     (ok4(d->res_ps, d->res_c0, d->res) && d->res_climit % (w16 ? 8 : 4) == 0 &&
+                      fit(d->res_ps, d->res_pl, d->res_c0 + d->ncols)));
     RDN_PROBE("conv3_ws_kernel<bf16,%d,%d%s%s>", BN, CK, d->gate ? ",gate" : "", ae ? ",ae" : "");
     if (d->gate) {
       if constexpr (NT % HU == 0) {
-        return ae ? launch_ws_k<BN, CK, true, true>(d, st, tiles_x, tiles_y, ntiles, cus)
-                  : launch_ws_k<BN, CK, true, false>(d, st, tiles_x, tiles_y, ntiles, cus);
+        if constexpr (BN > 80) {
+          return launch_ws_k<BN, CK, true, false>(d, st, tiles_x, tiles_y, ntiles, cus);
+        } else {
+          return ae ? launch_ws_k<BN, CK, true, true>(d, st, tiles_x, tiles_y, ntiles, cus)
+                    : launch_ws_k<BN, CK, true, false>(d, st, tiles_x, tiles_y, ntiles, cus);
+        }
       } else {
         return 1;
       }

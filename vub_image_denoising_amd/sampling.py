@@ -112,3 +112,35 @@ class SamplerGraph:
             packs.refresh()
         self.graph.replay()
         return self.out
+
+
+class ForwardGraph:
+    """hipGraph capture of one network forward for a fixed input shape: the plain
+    ``RDUNet`` (UNet/RDUNet_model.py:157-186) or ``RDUNet_T`` with a fixed t map --
+    the ~70 conv launches of a forward as one host launch (a batch-1 forward at
+    64x64 or 256x256 is launch-bound when issued eagerly)."""
+
+    def __init__(self, net, shape, t=None):
+        self.net = net
+        dev = next(net.parameters()).device
+        self.inp = torch.zeros(shape, dtype=torch.float32, device=dev)
+        self.t = None if t is None else t.to(dev)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.no_grad(), torch.cuda.stream(s):
+            for _ in range(2):   # engines, packs and workspaces allocated outside the capture
+                self._body()
+        torch.cuda.current_stream().wait_stream(s)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.no_grad(), torch.cuda.graph(self.graph):
+            self.out = self._body()
+
+    def _body(self):
+        return self.net(self.inp) if self.t is None else self.net(self.inp, self.t)
+
+    def __call__(self, x):
+        self.inp.copy_(x)
+        for packs in self.net._rdn_packs.values():   # weights changed since capture -> repack first
+            packs.refresh()
+        self.graph.replay()
+        return self.out
