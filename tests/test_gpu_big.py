@@ -79,6 +79,11 @@ CASES = [
     ("L1_conv1_dgrad_bn96_accum", 16, 128, 128, 32, 32, 0, 0, 96, 96, 0, 32, None, False, True),
     ("L1_conv2_fwd_bn32_planar", 16, 128, 128, 128, 160, 0, 32, 32, 160, 128, 32, None, False, False),
     ("L1_conv0_fwd_bn32_planar", 16, 128, 128, 64, 160, 0, 32, 32, 160, 64, 32, None, False, False),
+    # 4-wave blocks, two per CU (",w4": 64-column items on 32-channel chunks): the
+    # level-1 conv_3 forward, a ragged grid of it and the level-1 conv_0 input gradient
+    ("L1_conv3_fwd_ck32_w4", 16, 128, 128, 160, 160, 0, 32, 64, 64, 0, 0, (160, 0, 64), False, False),
+    ("L1_ragged_fwd_ck32_w4", 29, 72, 120, 160, 160, 0, 32, 64, 64, 0, 0, (160, 0, 64), False, False),
+    ("L1_conv0_dgrad_ck32_w4", 16, 128, 128, 32, 32, 0, 0, 64, 160, 0, 32, None, False, True),
 ]
 # gated input gradients are not taken by conv3_big (they stay on conv3_halo)
 GATED = ("L3_gated_dgrad", 8, 32, 32, 256, 256, 0, 0, 640, 640, 0, 128, None, True, True)
@@ -144,6 +149,7 @@ def test_conv3_big_vs_halo_and_torch(case):
     y_halo, k_halo = _run(case, True, ops)
     print(f"{name}: default -> {k_big}; override -> {k_halo}")
     assert k_big.startswith("conv3_halo_kernel" if gate else "conv3_big_kernel"), k_big
+    assert (",w4>" in k_big) == name.endswith("_w4"), k_big
     assert k_halo.startswith("conv3_halo_kernel"), k_halo
     # torch fp32 reference on the bf16 operands
     xs = x.nchw(N, Hh, Ww, xc0, cin)

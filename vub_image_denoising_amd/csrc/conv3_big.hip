@@ -73,7 +73,6 @@ __device__ __forceinline__ unsigned lds_addr(const unsigned char* p) {
   return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) unsigned char*)p;
 }
 
-constexpr int NTB = 512;
 constexpr int TWB = 16;
 constexpr int RS = TWB + 2;        // halo pixels per halo row
 constexpr int LDS_CAP = 160 * 1024;
@@ -89,8 +88,12 @@ __device__ __forceinline__ int hswz(int u, int x) {
   return CK == 64 ? (u ^ (x & 7)) : (u ^ ((x >> 1) & 3));
 }
 
-template <int TH, int BN, int WM, int CK>
+// NW waves per block: 8 = one block per CU (the LDS-heavy shapes); 4 = a 4-wave block
+// with half the LDS budget, two blocks per CU (see conv3_big_kernel's note on BIG_NW4)
+template <int TH, int BN, int WM, int CK, int NW = 8>
 struct PtCfg {
+  static constexpr int NTB = 64 * NW;
+  static constexpr int BPC = NW == 8 ? 1 : 2;                  // blocks per CU
   static constexpr int BM = TH * TWB;
   static constexpr int HWP = (TH + 2) * RS;                    // halo pixels
   static constexpr int RB = CK * 2;                            // bytes per halo pixel
@@ -102,14 +105,14 @@ struct PtCfg {
   static constexpr int RW = 256;                                // LDS weight row: 2 x 128 B
   static constexpr int W_BYTES = BN * RW;
   static constexpr int W_PIECES = W_BYTES / 1024;
-  static constexpr int W_PW = (W_PIECES + 7) / 8;               // weight pieces per wave per stage (max)
+  static constexpr int W_PW = (W_PIECES + NW - 1) / NW;         // weight pieces per wave per stage (max)
   static constexpr int TAB = 2 * COL_MAX * 4;
   static constexpr int LDS = 2 * HALO_BYTES + 2 * W_BYTES + TAB;
-  static constexpr int WN = 8 / WM;
+  static constexpr int WN = NW / WM;
   static constexpr int WTM = BM / WM, WTN = BN / WN;            // wave tile (pixels x columns)
   static constexpr int MT = WTM / 16, NTL = WTN / 16;
-  static constexpr bool OK = LDS <= LDS_CAP && MT >= 1 && NTL >= 1 && WTM % 16 == 0 && WTN % 16 == 0 &&
-                             (CK == 32 || CK == 64) && WM * WN == 8;
+  static constexpr bool OK = BPC * LDS <= LDS_CAP && MT >= 1 && NTL >= 1 && WTM % 16 == 0 && WTN % 16 == 0 &&
+                             (CK == 32 || CK == 64) && WM * WN == NW && (NW == 8 || NW == 4);
 };
 
 template <int NLO, int NHI, int SPLIT>
@@ -125,9 +128,19 @@ __device__ __forceinline__ void wait_split(int wave) {   // vmcnt(wave < SPLIT ?
 // (profiles/r04_final_conv3_big_resources.txt): 139-251 VGPRs, no scratch, except the
 // 128-column CK=64 items at 253-255 VGPRs, four of which (EP=1; EP=2..4 with GO) spill
 // 20-36 B/lane -- the next register cut is there (a 128-column wave tile split)
-template <int TH, int BN, int WM, int CK, int EP, bool GO>
-__global__ __launch_bounds__(NTB, 2) void conv3_big_kernel(rdn_conv_desc d, int tiles_x, int tiles_y, int nitems) {
-  using Cfg = PtCfg<TH, BN, WM, CK>;
+//
+// BIG_NW4 (round 5): at one 8-wave block per CU every wave reaches the same phase at
+// the same time -- the LDS-DMA issue after a barrier, the stage barriers, the item's
+// epilogue -- and the MFMA pipe idles through all of them.  Diagnostic builds on the
+// level-1 conv_3 forward (160 -> 64, B16, scripts/kbench.py, profiles/r05_bigdiag_kbench.txt):
+// 65.1 us as built; 44.6 without the in-loop DMAs, 51.9 without the epilogue, 53.0
+// without the stage waits + barriers, 25.0 with the MFMAs alone.  The 4-wave variant
+// (64 x 64 wave tiles) runs two independent blocks per CU, so one block's DMA issue,
+// barrier skew and epilogue overlap the other's MFMAs
+template <int TH, int BN, int WM, int CK, int EP, bool GO, int NW = 8>
+__global__ __launch_bounds__(64 * NW, 2) void conv3_big_kernel(rdn_conv_desc d, int tiles_x, int tiles_y, int nitems) {
+  using Cfg = PtCfg<TH, BN, WM, CK, NW>;
+  constexpr int NTB = Cfg::NTB;
   constexpr int RB = Cfg::RB, RW = Cfg::RW, SPC = Cfg::SPC, SS = Cfg::SS;
   constexpr int WTN = Cfg::WTN, MT = Cfg::MT, NTL = Cfg::NTL, W_PW = Cfg::W_PW, HP = Cfg::H_PIECES;
   constexpr bool FWD = EP == EP_FWD || EP == EP_FWD_RES;
@@ -186,8 +199,8 @@ __global__ __launch_bounds__(NTB, 2) void conv3_big_kernel(rdn_conv_desc d, int 
     const unsigned dst = lds_addr(halo) + hb * Cfg::HALO_BYTES;
     const bf16* const xb = (const bf16*)d.x + (((int64_t)q.nimg * H + (q.y0 - 1)) * W + (q.x0 - 1)) * d.x_ps;
 #pragma unroll
-    for (int k = 0; k < (HP + 7) / 8; ++k) {
-      const int pc = wave + 8 * k;
+    for (int k = 0; k < (HP + NW - 1) / NW; ++k) {
+      const int pc = wave + NW * k;
       if (pc >= HP) break;   // wave-uniform
       const int off = pc * 1024 + lane * 16;
       const int hp = off / RB, pu = (off % RB) / 16;
@@ -208,7 +221,7 @@ __global__ __launch_bounds__(NTB, 2) void conv3_big_kernel(rdn_conv_desc d, int 
     const unsigned dst = lds_addr(wst) + wb * Cfg::W_BYTES;
 #pragma unroll
     for (int k = 0; k < W_PW; ++k) {
-      const int pc = wave + 8 * k;                     // piece: rows 4 pc .. 4 pc + 3
+      const int pc = wave + NW * k;                    // piece: rows 4 pc .. 4 pc + 3
       if (pc >= Cfg::W_PIECES) break;                  // wave-uniform
       const int row = 4 * pc + (lane >> 4);
       const int u = (lane & 15) ^ (row & 15);
@@ -249,6 +262,13 @@ __global__ __launch_bounds__(NTB, 2) void conv3_big_kernel(rdn_conv_desc d, int 
     auto valid = [&](int q) { return 2 * jj + (q >> 1) < SPC && (2 * jj + (q >> 1)) * 64 + (q & 1) * 32 < 9 * CK; };
     u32x4 af[2][MT], bfr[2][NTL];
     auto rd = [&](int q, int buf) {
+#ifdef BIG_DIAG_NO_LDS   // diagnostic build (timing only): opaque fragments, no LDS reads
+#pragma unroll
+      for (int i = 0; i < MT; ++i) asm volatile("" : "=v"(af[buf][i]));
+#pragma unroll
+      for (int jn = 0; jn < NTL; ++jn) asm volatile("" : "=v"(bfr[buf][jn]));
+      return;
+#endif
       const int k0 = (2 * jj + (q >> 1)) * 64 + (q & 1) * 32;
       const int tap = k0 / CK, ksub = (k0 - tap * CK) / 32;
       const int dy = tap / 3, dx = tap % 3;
@@ -264,6 +284,13 @@ __global__ __launch_bounds__(NTB, 2) void conv3_big_kernel(rdn_conv_desc d, int 
       if (!valid(q)) break;
       if (q + 1 < 4 && valid(q + 1)) rd(q + 1, (q + 1) & 1);
       __builtin_amdgcn_sched_barrier(0);   // next k-step's reads issued before these MFMAs
+#ifdef BIG_DIAG_NO_MFMA   // diagnostic build (timing only): fragments consumed without MFMAs
+#pragma unroll
+      for (int i = 0; i < MT; ++i) asm volatile("" ::"v"(af[q & 1][i]));
+#pragma unroll
+      for (int jn = 0; jn < NTL; ++jn) asm volatile("" ::"v"(bfr[q & 1][jn]));
+      continue;
+#endif
 #pragma unroll
       for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -557,23 +584,44 @@ __global__ __launch_bounds__(NTB, 2) void conv3_big_kernel(rdn_conv_desc d, int 
 #pragma unroll
       for (int jj = 0; jj < SS; ++jj) {
         const bool nxt = jj + 1 < SS || more || has_next;
+#ifdef BIG_DIAG_NO_DMA   // diagnostic build (timing only): the prologue's stage and halo only
+        if (false) {
+#else
         if (nxt) {
+#endif
           if (jj + 1 < SS) issue_w(cur.n0, c, jj + 1, wbuf ^ 1);
           else if (more) issue_w(cur.n0, c + 1, 0, wbuf ^ 1);
           else issue_w(nq.n0, 0, 0, wbuf ^ 1);
         }
+#ifdef BIG_DIAG_NO_DMA
+        const bool hl = false;
+#else
         const bool hl = jj == 0 && (more || has_next);
+#endif
         if (hl) issue_h(more ? cur : nq, more ? c + 1 : 0, hbuf ^ 1);
         compute(jj, ph, wst + wbuf * Cfg::W_BYTES + b_lane);
-        if (hl && SS > 1) wait_split<HP / 8, HP / 8 + 1, HP % 8>(wave);   // weights landed; halo may fly
+#ifndef BIG_DIAG_NO_BAR   // diagnostic build (timing only): no per-stage wait and barrier
+        if (hl && SS > 1) wait_split<HP / NW, HP / NW + 1, HP % NW>(wave);   // weights landed; halo may fly
         else wait_vm<0>();
         __builtin_amdgcn_s_barrier();
+#endif
         asm volatile("" ::: "memory");
         wbuf ^= 1;
       }
       hbuf ^= 1;
     }
+#ifdef BIG_DIAG_NO_EPI   // diagnostic build (timing only): one conditional store keeps the accumulators live
+    {
+      float t = 0.f;
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int jn = 0; jn < NTL; ++jn) t += acc[i][jn][0] + acc[i][jn][3];
+      if (t == 1.2345f) ((float*)d.out)[tid] = t;
+    }
+#else
     epilogue(cur, item);   // global stores drain under the next item
+#endif
     item = nxt_item;
     cur = nq;
   }
@@ -610,13 +658,14 @@ int epi_mode(const rdn_conv_desc* d) {
   return -1;
 }
 
-template <int TH, int BN, int WM, int CK, int EP, bool GO = false>
+template <int TH, int BN, int WM, int CK, int EP, bool GO = false, int NW = 8>
 int launch_pt(const rdn_conv_desc* d, hipStream_t st, int tiles_x, int tiles_y, int nitems) {
-  if constexpr (!PtCfg<TH, BN, WM, CK>::OK) {
+  using Cfg = PtCfg<TH, BN, WM, CK, NW>;
+  if constexpr (!Cfg::OK) {
     return 1;
   } else {
     constexpr bool FWD_ = EP == EP_FWD || EP == EP_FWD_RES;
-    if constexpr (BIG_W16 && !(GO && !FWD_) && PtCfg<TH, BN, WM, CK>::MT % 2 == 0) {
+    if constexpr (BIG_W16 && !(GO && !FWD_) && Cfg::MT % 2 == 0) {
       // 16-byte epilogue units: 8-channel aligned operands
       auto a8 = [](int64_t ps, int64_t c0, const void* p) { return ps % 8 == 0 && c0 % 8 == 0 && !((uintptr_t)p & 15); };
       if (!a8(d->out_ps, d->out_c0, d->out)) return 1;
@@ -624,37 +673,39 @@ int launch_pt(const rdn_conv_desc* d, hipStream_t st, int tiles_x, int tiles_y, 
       if ((EP == EP_FWD_RES || EP == EP_RES) && (!a8(d->res_ps, d->res_c0, d->res) || d->res_climit % 8)) return 1;
     }
     if (GO) rdn_probe_rows = (int)((int64_t)d->n * tiles_x * tiles_y * WM);
-    RDN_PROBE("conv3_big_kernel<bf16,%d,%d,%d,%d%s>", TH, BN, WM, CK, GO ? ",go" : "");
+    RDN_PROBE("conv3_big_kernel<bf16,%d,%d,%d,%d%s%s>", TH, BN, WM, CK, GO ? ",go" : "", NW == 4 ? ",w4" : "");
     const int per_xcd = (nitems + 7) / 8;
-    int slots = cu_count() / 8;
+    int slots = Cfg::BPC * cu_count() / 8;   // blocks per XCD
     if (slots > per_xcd) slots = per_xcd;
     if (slots < 1) slots = 1;
-    hipLaunchKernelGGL((conv3_big_kernel<TH, BN, WM, CK, EP, GO>), dim3((unsigned)(8 * slots)), dim3(NTB), 0, st, *d,
-                       tiles_x, tiles_y, nitems);
+    hipLaunchKernelGGL((conv3_big_kernel<TH, BN, WM, CK, EP, GO, NW>), dim3((unsigned)(8 * slots)), dim3(Cfg::NTB), 0,
+                       st, *d, tiles_x, tiles_y, nitems);
     return rdn_check_launch("rdn_conv_fwd(conv3 big)");
   }
 }
 
-template <int TH, int BN, int WM, int CK>
+template <int TH, int BN, int WM, int CK, int NW = 8>
 int launch_big(const rdn_conv_desc* d, hipStream_t st) {
   const int tiles_x = (d->w + TWB - 1) / TWB, tiles_y = (d->h + TH - 1) / TH;
   const int64_t nitems = (int64_t)d->n * tiles_x * tiles_y * (d->ncols / BN);
   if (nitems >= (1ll << 31)) return 1;
   const int ni = (int)nitems;
-  if (d->gout) {   // gate-out: the input-gradient modes only
-    switch (epi_mode(d)) {
-      case EP_PLAIN: return launch_pt<TH, BN, WM, CK, EP_PLAIN, true>(d, st, tiles_x, tiles_y, ni);
-      case EP_ACC: return launch_pt<TH, BN, WM, CK, EP_ACC, true>(d, st, tiles_x, tiles_y, ni);
-      case EP_RES: return launch_pt<TH, BN, WM, CK, EP_RES, true>(d, st, tiles_x, tiles_y, ni);
+  if (d->gout) {   // gate-out: the input-gradient modes only (8-wave blocks: the 4-wave ones spill)
+    if constexpr (NW == 8) {
+      switch (epi_mode(d)) {
+        case EP_PLAIN: return launch_pt<TH, BN, WM, CK, EP_PLAIN, true>(d, st, tiles_x, tiles_y, ni);
+        case EP_ACC: return launch_pt<TH, BN, WM, CK, EP_ACC, true>(d, st, tiles_x, tiles_y, ni);
+        case EP_RES: return launch_pt<TH, BN, WM, CK, EP_RES, true>(d, st, tiles_x, tiles_y, ni);
+      }
     }
     return 1;
   }
   switch (epi_mode(d)) {
-    case EP_FWD: return launch_pt<TH, BN, WM, CK, EP_FWD>(d, st, tiles_x, tiles_y, ni);
-    case EP_FWD_RES: return launch_pt<TH, BN, WM, CK, EP_FWD_RES>(d, st, tiles_x, tiles_y, ni);
-    case EP_PLAIN: return launch_pt<TH, BN, WM, CK, EP_PLAIN>(d, st, tiles_x, tiles_y, ni);
-    case EP_ACC: return launch_pt<TH, BN, WM, CK, EP_ACC>(d, st, tiles_x, tiles_y, ni);
-    case EP_RES: return launch_pt<TH, BN, WM, CK, EP_RES>(d, st, tiles_x, tiles_y, ni);
+    case EP_FWD: return launch_pt<TH, BN, WM, CK, EP_FWD, false, NW>(d, st, tiles_x, tiles_y, ni);
+    case EP_FWD_RES: return launch_pt<TH, BN, WM, CK, EP_FWD_RES, false, NW>(d, st, tiles_x, tiles_y, ni);
+    case EP_PLAIN: return launch_pt<TH, BN, WM, CK, EP_PLAIN, false, NW>(d, st, tiles_x, tiles_y, ni);
+    case EP_ACC: return launch_pt<TH, BN, WM, CK, EP_ACC, false, NW>(d, st, tiles_x, tiles_y, ni);
+    case EP_RES: return launch_pt<TH, BN, WM, CK, EP_RES, false, NW>(d, st, tiles_x, tiles_y, ni);
   }
   return 1;
 }
@@ -680,6 +731,19 @@ bool big_ck32_multi() {
   static const bool on = [] {
     const char* e = getenv("RDN_BIG_CK32");
     return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// RDN_BIG_NW4=0: the 64-column 32-channel-chunk items on 8-wave blocks (A/B)
+bool big_nw4() {
+  static const bool on = [] {
+    const char* e = getenv("RDN_BIG_NW4");
+#ifdef BIG_NW4_OFF   // variant build for in-process A/B (scripts/kbench.py)
+    return e && e[0] == '1';
+#else
+    return !(e && e[0] == '0');
+#endif
   }();
   return on;
 }
@@ -732,7 +796,12 @@ int big_dispatch(const rdn_conv_desc* d, hipStream_t st) {
     // interleaved, r04_v18_big_fall_ab.txt): off, RDN_BIG_FALL=1 for A/B
     if (!(big_fall() && d->ncols % 64 == 0 && tiles * (d->ncols / 64) <= 6ll * cus)) return 1;
   }
-  if (d->ncols % 64 == 0) return narrow_ok(64) ? launch_big<16, 64, 4, CK>(d, st) : 1;
+  if (d->ncols % 64 == 0) {
+    if (!narrow_ok(64)) return 1;
+    if constexpr (CK == 32)   // two 4-wave blocks per CU (79 KB of LDS each), 64 x 64 wave tiles
+      if (big_nw4() && !d->gout) return launch_big<16, 64, 4, CK, 4>(d, st);
+    return launch_big<16, 64, 4, CK>(d, st);
+  }
   if (d->ncols == 32) {
     // the narrow level-1 forwards (64 / 128 input channels -> 32; 32 x 32 wave tiles,
     // near the HBM ridge): per-layer A/B at B16, conv_0 28 -> 26 us (was conv3_wsd),
