@@ -254,11 +254,10 @@ __global__ __launch_bounds__(64 * NW, 2) void conv3_big_kernel(rdn_conv_desc d, 
       for (int jn = 0; jn < NTL; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
   };
 
-#if BIG_PF
   // LDS stage jj of a chunk (K stages 2jj, 2jj+1) from halo image ph, weights pbs, as a
   // pipeline over its (up to) four 32-deep k-steps: the fragments of k-step q + 1 are
   // read before the MFMAs of q (two fragment sets live; same MFMA order: bit-identical)
-  auto compute = [&](int jj, const unsigned char* ph, const unsigned char* pbs) {
+  auto compute_pf = [&](int jj, const unsigned char* ph, const unsigned char* pbs) {
     auto valid = [&](int q) { return 2 * jj + (q >> 1) < SPC && (2 * jj + (q >> 1)) * 64 + (q & 1) * 32 < 9 * CK; };
     u32x4 af[2][MT], bfr[2][NTL];
     auto rd = [&](int q, int buf) {
@@ -300,9 +299,49 @@ __global__ __launch_bounds__(64 * NW, 2) void conv3_big_kernel(rdn_conv_desc d, 
                                                                0, 0);
     }
   };
-#else
-  // LDS stage jj of a chunk (K stages 2jj, 2jj+1) from halo image ph, weights pbs
-  auto compute = [&](int jj, const unsigned char* ph, const unsigned char* pbs) {
+  // rolling form of the prefetch: the next k-step's weight fragments are read before
+  // the MFMAs (double-buffered), each pixel fragment i of it right after the MFMAs that
+  // read fragment i of this k-step (one buffer: MT x 4 fewer live registers; same MFMA
+  // order, bit-identical)
+  auto compute_roll = [&](int jj, const unsigned char* ph, const unsigned char* pbs) {
+    auto valid = [&](int q) { return 2 * jj + (q >> 1) < SPC && (2 * jj + (q >> 1)) * 64 + (q & 1) * 32 < 9 * CK; };
+    u32x4 af[MT], bfr[2][NTL];
+    auto pa_of = [&](int q) {
+      const int k0 = (2 * jj + (q >> 1)) * 64 + (q & 1) * 32;
+      const int tap = k0 / CK, ksub = (k0 - tap * CK) / 32;
+      const int dy = tap / 3, dx = tap % 3;
+      return ph + a_row0 + dy * RS * RB + a_off[ksub * 3 + dx];
+    };
+    auto rdb = [&](int q, int buf) {
+#pragma unroll
+      for (int jn = 0; jn < NTL; ++jn) bfr[buf][jn] = *(const u32x4*)(pbs + jn * 16 * RW + b_off[q]);
+    };
+    {
+      const unsigned char* pa = pa_of(0);
+#pragma unroll
+      for (int i = 0; i < MT; ++i) af[i] = *(const u32x4*)(pa + i * RS * RB);
+      rdb(0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (!valid(q)) break;
+      const bool nx = q + 1 < 4 && valid(q + 1);
+      if (nx) rdb(q + 1, (q + 1) & 1);
+      const unsigned char* pn = pa_of(nx ? q + 1 : q);
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int jn = 0; jn < NTL; ++jn)   // D[column][pixel]
+          acc[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bfr[q & 1][jn]),
+                                                               __builtin_bit_cast(bf16x8, af[i]), acc[i][jn], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);   // (the reload may not move above the MFMAs reading af[i])
+        if (nx) af[i] = *(const u32x4*)(pn + i * RS * RB);
+      }
+    }
+  };
+  // the same without the k-step prefetch: one fragment set live at a time
+  auto compute_np = [&](int jj, const unsigned char* ph, const unsigned char* pbs) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int j = 2 * jj + h;
@@ -330,7 +369,23 @@ __global__ __launch_bounds__(64 * NW, 2) void conv3_big_kernel(rdn_conv_desc d, 
       }
     }
   };
+  // ROLL: the rolling prefetch where the full second fragment set spilled, the 128-column
+  // 64-channel-chunk residual-forward and gate-out items (12-36 B/lane at 255 VGPRs,
+  // round 4; without any prefetch they run 4-7 % longer, profiles/r05_spill_*)
+#ifdef BIG_PF_ALL   // variant build for A/B: the round-4 rule (prefetch everywhere)
+  constexpr bool ROLL = false;
+#else
+  constexpr bool ROLL = BIG_PF && BN == 128 && CK == 64 && (GOK || EP == EP_FWD_RES);
 #endif
+  // (the gate-out residual form, which the train step does not launch, spills even so:
+  // no prefetch there)
+  constexpr bool NOPF = BN == 128 && CK == 64 && GOK && EP == EP_RES;
+  auto compute = [&](int jj, const unsigned char* ph, const unsigned char* pbs) {
+    if constexpr (NOPF) compute_np(jj, ph, pbs);
+    else if constexpr (ROLL) compute_roll(jj, ph, pbs);
+    else if constexpr (BIG_PF) compute_pf(jj, ph, pbs);
+    else compute_np(jj, ph, pbs);
+  };
 
   // ---- epilogue: straight from the accumulators, through buffer descriptors on the
   // item's first pixel (32-bit offsets: few registers; pixels past the image edge get

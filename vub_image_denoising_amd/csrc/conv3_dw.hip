@@ -82,6 +82,14 @@ constexpr int NT = 512;   // 8 waves
 #ifndef DW_SB
 #define DW_SB 1      // one barrier per tile (dY and X halos double-buffered in LDS)
 #endif
+#ifndef DW_GP_LATE
+// gate-out: 1 = the finished layer's PReLU input loaded after the dgrad MFMAs (its
+// latency exposed, 16 fewer live registers), 0 (default) = before them; -1 = after them
+// on the 64-column single-part shape only, which spills 12 B/lane the other way -- but
+// runs 4-7 % longer per launch without the spill (level-1 conv_0, B16 / B32 layer
+// reports, profiles/r05_spill_layers.txt): the spill stays
+#define DW_GP_LATE 0
+#endif
 #ifndef DW_DPF
 #define DW_DPF 0     // dgrad: next k-step's fragments read before the current MFMAs (A/B)
 #endif
@@ -419,7 +427,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       // MFMAs (prefetched a tile ahead beside `eo` instead: up_0.conv 227 -> 240 us,
       // the level-1 conv_0 spilled)
       u32x2 gp[GO ? MT : 1][GO ? NTL : 1];
-      if constexpr (GO) {
+      auto load_gp = [&]() {
         int oy, ox, on;
         origin(tt, oy, ox, on);
         const __amdgpu_buffer_rsrc_t rp =
@@ -429,7 +437,9 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
 #pragma unroll
           for (int jn = 0; jn < NTL; ++jn)
             gp[i][jn] = rdn_ld8(rp, gon[jn], (((2 * rw + i) * W + r) * (int)d.gout_pre_ps + coff_g[jn]) * 2);
-      }
+      };
+      constexpr bool GP_LATE = DW_GP_LATE == 1 || (DW_GP_LATE < 0 && BN == 64 && NH == 1);
+      if constexpr (GO && !GP_LATE) load_gp();
       auto aoff_of = [&](int j) {
         if constexpr (KALIGN) {
           const int k0 = 32 * j;
@@ -483,6 +493,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
 #ifdef DW_STAMPS
       st_mid = DW_NOW();
 #endif
+      if constexpr (GO && GP_LATE) load_gp();
       int oy, ox, on;
       origin(tt, oy, ox, on);
       bf16* const ob = (bf16*)d.out + (((int64_t)on * H + oy) * W + ox) * d.out_ps;

@@ -158,25 +158,37 @@ __global__ __launch_bounds__(NT_MAX) void image_metrics_kernel(const float* __re
   }
 }
 
-// one thread per image: channels and tiles summed in a fixed order
-__global__ void image_metrics_final_kernel(const double* __restrict__ part, int N, int C, int H, int W, int tiles,
-                                           double range, double* __restrict__ psnr, double* __restrict__ ssim) {
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
-  double se = 0.0, s_img = 0.0;
-  const double interior = (double)(H - 2 * R) * (double)(W - 2 * R);
-  for (int c = 0; c < C; ++c) {
-    double sc = 0.0;
-    for (int t = 0; t < tiles; ++t) {
-      const int64_t slot = ((int64_t)n * C + c) * tiles + t;
-      se += part[2 * slot];
-      sc += part[2 * slot + 1];
-    }
-    s_img += sc / interior;
+// one block per image: thread t sums slots t, t + 256, ... of the image's C x tiles
+// partials, then a fixed shared-memory tree (deterministic).  (One thread per image
+// looping over its slots waits on C x tiles dependent loads.)
+__global__ __launch_bounds__(256) void image_metrics_final_kernel(const double* __restrict__ part, int C, int H,
+                                                                  int W, int tiles, double range,
+                                                                  double* __restrict__ psnr, double* __restrict__ ssim) {
+  __shared__ double red[2][256];
+  const int n = blockIdx.x, t = threadIdx.x;
+  const int slots = C * tiles;
+  double se = 0.0, sc = 0.0;
+  for (int k = t; k < slots; k += 256) {
+    const int64_t slot = (int64_t)n * slots + k;
+    se += part[2 * slot];
+    sc += part[2 * slot + 1];
   }
-  const double mse = se / ((double)C * H * W);
-  if (psnr) psnr[n] = 10.0 * log10(range * range / mse);   // mse == 0 -> inf, as skimage
-  if (ssim) ssim[n] = s_img / C;
+  red[0][t] = se;
+  red[1][t] = sc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o) {
+      red[0][t] += red[0][t + o];
+      red[1][t] += red[1][t + o];
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    const double interior = (double)(H - 2 * R) * (double)(W - 2 * R);
+    const double mse = red[0][0] / ((double)C * H * W);
+    if (psnr) psnr[n] = 10.0 * log10(range * range / mse);   // mse == 0 -> inf, as skimage
+    if (ssim) ssim[n] = red[1][0] / interior / C;
+  }
 }
 
 // rows per block: fewer, taller tiles measured faster than a fuller grid of short
@@ -212,6 +224,6 @@ extern "C" int rdn_image_metrics(const float* gt, const float* x, int32_t n, int
   const float cov_norm = (float)(WIN * WIN) / (float)(WIN * WIN - 1);
   image_metrics_kernel<<<dim3(tiles, c, n), ct.nt, 0, (hipStream_t)stream>>>(gt, x, c, h, w, ct.n, ct.txo, ty, c1, c2,
                                                                              cov_norm, ws);
-  image_metrics_final_kernel<<<(n + 63) / 64, 64, 0, (hipStream_t)stream>>>(ws, n, c, h, w, tiles, rr, psnr, ssim);
+  image_metrics_final_kernel<<<n, 256, 0, (hipStream_t)stream>>>(ws, c, h, w, tiles, rr, psnr, ssim);
   return rdn_check_launch("rdn_image_metrics");
 }
