@@ -49,6 +49,9 @@ constexpr int TH = 8, TW = 16, TP = TH * TW;
 constexpr int HW_ = TW + 2, HP = (TH + 2) * HW_;
 constexpr int LDS_MAX = 160 * 1024;
 
+#ifndef WG_NW4
+#define WG_NW4 0    // 1: the 64 x 64 shape on 4-wave blocks (64 x 144 wave tiles)
+#endif
 #ifndef WG_PIPE
 #define WG_PIPE 0   // B-fragment prefetch depth of the (k-step, n-tile) pipeline; 0: the r03 form
 #endif
@@ -64,7 +67,7 @@ struct Geo {
   // every shape fits two waves per SIMD -- bit-identical, but 1-6 % slower per launch
   // on 5 of the 7 train-step shapes and -0.5 % on the step (profiles/r04_v4_wgrad_pipe_*):
   // kept as the WG_PIPE=n variant, off
-  static constexpr int NW = ((WG_PIPE > 0 && BM >= 32 && !(BM == 64 && CK == 96)) || (BM == 64 && CK == 64)) ? 8 : 4,
+  static constexpr int NW = ((WG_PIPE > 0 && BM >= 32 && !(BM == 64 && CK == 96)) || (BM == 64 && CK == 64 && !WG_NW4)) ? 8 : 4,
                        NTH = 64 * NW;   // (64 x 96: 78 VGPRs of spill at two waves per SIMD)
   static constexpr int NCOL = 9 * CK, NT_ALL = (NCOL + 15) / 16;
   // waves as WMv (along M) x WNv (along the 9*CK columns), the same number of
