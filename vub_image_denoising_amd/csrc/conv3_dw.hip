@@ -93,6 +93,12 @@ constexpr int NT = 512;   // 8 waves
 #ifndef DW_DPF
 #define DW_DPF 0     // dgrad: next k-step's fragments read before the current MFMAs (A/B)
 #endif
+#ifndef DW_WSHARE
+// 1: on the one-barrier (SB) shapes the W waves load and gate the last partial round
+// of the dY halo units ([(D_IT - 1) * 256, D_UNITS)), which the D waves did -- the D
+// waves are the critical path of a tile, the W waves waited at its barrier (round 5)
+#define DW_WSHARE 1
+#endif
 #ifndef DW_W16
 #define DW_W16 1     // dX epilogue in 16-byte units (lane-row swap); 0: 8-byte units (A/B)
 #endif
@@ -116,7 +122,14 @@ struct DwCfg {
   static constexpr int D_BYTES = (HW_ * DROW + 15) / 16 * 16;
   static constexpr int X_BYTES = (HW_ * XROW + 15) / 16 * 16;
   static constexpr int CT_BYTES = 0;                    // dX leaves from the accumulators
-  static constexpr int RED_BYTES = 2 * 256 * 8 * 4;     // dalpha/dbias partial reduction (aliases)
+  static constexpr bool SB_ = DW_SB && !((BN == 64 && CK == 16) || (BN == 32 && CK == 32));
+  // W waves gate the dY halo ring (BSPLIT below) on the level-0 shapes: per launch at B16
+  // (scripts/dw_kbench.py, profiles/r05_wsh_kbench_ab.txt) 32->16 57.0 -> 55.0 us, 80->32
+  // 136.4 -> 133.5, up_0.conv (h2, go) 243.9 -> 208.5; the level-1 shapes ran 1-2 us slower
+  // with it (64->32 34.1 -> 35.6, h2 46.8 / 52.9 -> 47.7 / 54.4, go 46.5 -> 48.9) and h5
+  // even: off there
+  static constexpr bool WSH = DW_WSHARE && SB_ && (CK == 16 || BN == 80 || (GO && BN == 48));
+  static constexpr int RED_BYTES = 2 * (WSH ? 512 : 256) * 8 * 4;   // dalpha/dbias partial reduction (aliases)
   static constexpr int AL_BYTES = (CK * 4 + 15) / 16 * 16;   // gate slopes
   static constexpr int GAL_BYTES = GO ? BN * 4 : 0;           // gate-out: the finished layer's slopes
   // W waves keep two X halos in flight in registers where the budget allows it
@@ -129,7 +142,7 @@ struct DwCfg {
   // pass overlapping the W waves' MFMAs (per launch, profiles/r03_v15_dw_sb_kbench:
   // 32->16 59 -> 54 us, 80->32 135 -> 133, 64->32 36 -> 34; the 64->16 and 32->32
   // shapes ran 1-3 us slower and keep two barriers per tile)
-  static constexpr bool SB = DW_SB && !((BN == 64 && CK == 16) || (BN == 32 && CK == 32));
+  static constexpr bool SB = SB_;
   static constexpr int DB = SB ? 2 : 1;
   static constexpr int BASE = W_BYTES + DB * D_BYTES + CT_BYTES + AL_BYTES + GAL_BYTES;
   // X halo buffers in LDS: 2 for the LDS double buffer, 1 where it would not fit
@@ -141,7 +154,7 @@ struct DwCfg {
   // vmcnt(0) at the loop head, i.e. on the previous tile's dX stores)
   static constexpr int DUMP_BYTES = 256 * 16;
   static constexpr int LDS = BASE + XB * X_BYTES + DUMP_BYTES;
-  static constexpr bool FITS = LDS <= LDS_MAX && D_BYTES + X_BYTES + CT_BYTES >= RED_BYTES &&
+  static constexpr bool FITS = LDS <= LDS_MAX && DB * D_BYTES + XB * X_BYTES + CT_BYTES >= RED_BYTES &&
                               (!GO || W_BYTES >= 8 * BN * 4);   // gate-out partials in the dead panel
 };
 
@@ -158,6 +171,18 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
   constexpr int DU = CK / VEC, XU = BN / VEC;           // 16-B units per halo pixel
   constexpr int D_UNITS = HW_ * DU, X_UNITS = HW_ * XU;
   constexpr int D_IT = (D_UNITS + NR - 1) / NR, X_IT = (X_UNITS + NR - 1) / NR;
+  // dY halo units of the D waves: all, or (WSH) all but the last partial round [DN, D_UNITS),
+  // which the W waves take (one unit per W thread)
+  constexpr bool WSH = Cfg::WSH;
+  // BSPLIT: the D waves take exactly the tile-interior units (TH x TW pixels: 1 or 2
+  // whole rounds at 16 / 32 dY channels) and the W waves the halo ring (52 pixels), so
+  // only the D waves count dalpha / dbias partials and the W waves gate with the packed
+  // form (no partial registers: the 80-column W waves spilled with them)
+  constexpr int IU = TH * TW * DU;
+  constexpr bool BSPLIT = WSH && IU % NR == 0 && D_UNITS - IU <= NR;
+  constexpr int D_ITD = BSPLIT ? IU / NR : WSH ? D_IT - 1 : D_IT, DN = D_ITD * NR;
+  constexpr int RED_T = WSH ? 2 * NR : NR;              // threads with dalpha/dbias partials
+  static_assert(!WSH || (D_ITD >= 1 && D_UNITS - DN <= NR), "W share geometry");
   constexpr int MTW = CK / 16;                          // wgrad m-tiles
   constexpr int NT_ALL = 9 * BN / 16;                   // wgrad n-tiles
   constexpr int NTW = (NT_ALL + 3) / 4;                 // per W wave (n-tile = wave + 4 j)
@@ -248,12 +273,13 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
   if (dwave) {
     // ================= D waves: gated dY halo, dgrad, dX epilogue
     const int dcu = rt % DU;
-    int lrel[D_IT], grel[D_IT], llds[D_IT], uhp[D_IT];
+    int lrel[D_ITD], grel[D_ITD], llds[D_ITD], uhp[D_ITD];
     unsigned dint = 0;   // bit it: unit `it` is a tile-interior pixel (counted in the partials)
 #pragma unroll
-    for (int it = 0; it < D_IT; ++it) {
+    for (int it = 0; it < D_ITD; ++it) {
       const int u = rt + it * NR;
-      const int hp = u < D_UNITS ? u / DU : HW_;
+      int hp = u < D_UNITS ? u / DU : HW_;
+      if constexpr (BSPLIT) hp = (hp / TW + 1) * RS + hp % TW + 1;   // interior pixel u / DU
       const int hq = hp < HW_ ? hp : 0;
       const int hy = hq / RS, hx = hq - hy * RS;
       uhp[it] = hp;
@@ -304,14 +330,14 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
         gsa[jn][e] = 0.f;
         gsb[jn][e] = 0.f;
       }
-    auto load = [&](int tt, u32x4 (&lr)[D_IT], u32x4 (&gr)[D_IT]) {
+    auto load = [&](int tt, u32x4 (&lr)[D_ITD], u32x4 (&gr)[D_ITD]) {
       int oy, ox, on;
       origin(tt, oy, ox, on);
       const int64_t hpix0 = ((int64_t)on * H + (oy - 1)) * W + (ox - 1);
       const __amdgpu_buffer_rsrc_t rd = rdn_rsrc(DY + hpix0 * d.x_ps);
       const __amdgpu_buffer_rsrc_t rg = rdn_rsrc(GT ? PR + hpix0 * d.gate_ps : DY);
 #pragma unroll
-      for (int it = 0; it < D_IT; ++it) {
+      for (int it = 0; it < D_ITD; ++it) {
         const bool ok = in_img(uhp[it], oy, ox);
 #ifdef DW_DIAG_NO_LOAD
         lr[it] = u32x4{(unsigned)ok, 0u, 0u, 0u};
@@ -326,10 +352,10 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     };
     // registers -> LDS with the PReLU-backward gate and the dalpha/dbias partials of
     // the tile-interior pixels (each image pixel is interior to exactly one tile)
-    auto store = [&](const u32x4 (&lr)[D_IT], const u32x4 (&gr)[D_IT], bool live, int doff) {
+    auto store = [&](const u32x4 (&lr)[D_ITD], const u32x4 (&gr)[D_ITD], bool live, int doff) {
       if constexpr (!GT) {   // the operand is dYpre already (gate-out finisher / PReLU pass)
 #pragma unroll
-        for (int it = 0; it < D_IT; ++it)
+        for (int it = 0; it < D_ITD; ++it)
           *(u32x4*)(uhp[it] < HW_ ? dyh + doff + llds[it] : dump + rt * 16) = lr[it];
         return;
       }
@@ -341,7 +367,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       if (!live) {   // (block-uniform) no partials to count: the packed gate, ~half the VALU
 #endif
 #pragma unroll
-        for (int it = 0; it < D_IT; ++it) {
+        for (int it = 0; it < D_ITD; ++it) {
           u32x4 o;
           o[0] = rdn_gate2(lr[it][0], gr[it][0], a0[0], a0[1]);
           o[1] = rdn_gate2(lr[it][1], gr[it][1], a0[2], a0[3]);
@@ -353,7 +379,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       }
 #endif
 #pragma unroll
-      for (int it = 0; it < D_IT; ++it) {
+      for (int it = 0; it < D_ITD; ++it) {
         float dy[VEC], pr[VEC];
         Unit16<bf16>::unpack(lr[it], dy);
         Unit16<bf16>::unpack(gr[it], pr);
@@ -565,7 +591,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
         }
     };
 
-    u32x4 lA[D_IT], gA[D_IT], lB[D_IT], gB[D_IT];
+    u32x4 lA[D_ITD], gA[D_ITD], lB[D_ITD], gB[D_ITD];
     u32x2 eC[MT][NE], eN[MT][NE];
     if constexpr (Cfg::SB) {
     // step k computes tile t from buffer k&1 while it gates tile t + per (issued one
@@ -580,7 +606,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
                          // count the same ops on entry and on the back edge, not vmcnt(0))
     }
     __syncthreads();   // weights + first halos
-    auto step = [&](u32x4 (&lc)[D_IT], u32x4 (&gc)[D_IT], const u32x2 (&ec)[MT][NE], u32x2 (&en)[MT][NE],
+    auto step = [&](u32x4 (&lc)[D_ITD], u32x4 (&gc)[D_ITD], const u32x2 (&ec)[MT][NE], u32x2 (&en)[MT][NE],
                     int cur) -> bool {
       const int t1 = t + per;
 #ifdef DW_STAMPS
@@ -617,7 +643,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       load(min(t + per, t_last), lA, gA);
     }
     __syncthreads();   // weights + first halos
-    auto step = [&](u32x4 (&lc)[D_IT], u32x4 (&gc)[D_IT], u32x4 (&ln)[D_IT], u32x4 (&gn)[D_IT],
+    auto step = [&](u32x4 (&lc)[D_ITD], u32x4 (&gc)[D_ITD], u32x4 (&ln)[D_ITD], u32x4 (&gn)[D_ITD],
                     const u32x2 (&ec)[MT][NE], u32x2 (&en)[MT][NE]) -> bool {
       const int t1 = t + per;
       load(min(t + 2 * per, t_last), ln, gn);
@@ -659,7 +685,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
 #pragma unroll
       for (int k = 0; k < VEC; ++k) {
         red[rt * VEC + k] = sa[k];
-        red[NR * VEC + rt * VEC + k] = sb[k];
+        red[RED_T * VEC + rt * VEC + k] = sb[k];
       }
     }
   } else {
@@ -668,34 +694,130 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     const int xupp = (wg.b_pl && xc0 % wg.b_ps == 0 && XU % (wg.b_ps / VEC) == 0) ? (int)(wg.b_ps / VEC) : XU;
     // per unit: global offset and LDS offset (-1: padding unit; its halo pixel is
     // llds / XROW, so no third array)
-    int lrel[X_IT], llds[X_IT];
-#pragma unroll
-    for (int it = 0; it < X_IT; ++it) {
+    // (XREC: the two index arrays recomputed per use instead of held -- tried for the W
+    // share of the widest shape, it spilled more)
+    constexpr bool XREC = false;
+    auto xunit = [&](int it, int& rel, int& ll) {
       const int u = rt + it * NR;
       const int pln = u / (HW_ * xupp), rem = u - pln * (HW_ * xupp);
       const bool ok = u < X_UNITS;
       const int hq = ok ? rem / xupp : 0, cu = ok ? pln * xupp + rem % xupp : 0;
       const int hy = hq / RS, hx = hq - hy * RS;
-      lrel[it] = (hy * W + hx) * (int)wg.b_ps + rdn_coff32(xc0 + cu * VEC, (int)wg.b_ps, (int)wg.b_pl);
-      llds[it] = ok ? hq * XROW + cu * 16 : -1;
+      rel = (hy * W + hx) * (int)wg.b_ps + rdn_coff32(xc0 + cu * VEC, (int)wg.b_ps, (int)wg.b_pl);
+      ll = ok ? hq * XROW + cu * 16 : -1;
+    };
+    int lrel_[XREC ? 1 : X_IT], llds_[XREC ? 1 : X_IT];
+    if constexpr (!XREC) {
+#pragma unroll
+      for (int it = 0; it < X_IT; ++it) xunit(it, lrel_[it], llds_[it]);
     }
+    auto xrel = [&](int it) {
+      if constexpr (XREC) {
+        int rel, ll;
+        xunit(it, rel, ll);
+        return rel;
+      } else {
+        return lrel_[it];
+      }
+    };
+    auto xlds = [&](int it) {
+      if constexpr (XREC) {
+        int rel, ll;
+        xunit(it, rel, ll);
+        return ll;
+      } else {
+        return llds_[it];
+      }
+    };
     auto load = [&](int tt, u32x4 (&lr)[X_IT]) {
       int oy, ox, on;
       origin(tt, oy, ox, on);
       const int64_t hpix0 = ((int64_t)on * H + (oy - 1)) * W + (ox - 1);
       const __amdgpu_buffer_rsrc_t rx = rdn_rsrc(XS + hpix0 * wg.b_ps);
 #pragma unroll
-      for (int it = 0; it < X_IT; ++it)
+      for (int it = 0; it < X_IT; ++it) {
+        const int ll = xlds(it);
 #ifdef DW_DIAG_NO_LOAD
-        lr[it] = u32x4{(unsigned)in_img(llds[it] < 0 ? HW_ : llds[it] / XROW, oy, ox), 0u, 0u, 0u};
+        lr[it] = u32x4{(unsigned)in_img(ll < 0 ? HW_ : ll / XROW, oy, ox), 0u, 0u, 0u};
 #else
-        lr[it] = rdn_ld16(rx, in_img(llds[it] < 0 ? HW_ : llds[it] / XROW, oy, ox), lrel[it] * 2);
+        lr[it] = rdn_ld16(rx, in_img(ll < 0 ? HW_ : ll / XROW, oy, ox), xrel(it) * 2);
 #endif
+      }
     };
     auto store = [&](const u32x4 (&lr)[X_IT], int xoff) {
 #pragma unroll
-      for (int it = 0; it < X_IT; ++it)
-        *(u32x4*)(llds[it] >= 0 ? xh + xoff + llds[it] : dump + rt * 16) = lr[it];
+      for (int it = 0; it < X_IT; ++it) {
+        const int ll = xlds(it);
+        *(u32x4*)(ll >= 0 ? xh + xoff + ll : dump + rt * 16) = lr[it];
+      }
+    };
+    // (WSH) dY halo unit DN + rt: loaded, gated (the D waves' fast packed gate, or the
+    // scalar one with the dalpha/dbias partials of a tile-interior unit) and stored to
+    // the same LDS image as the D waves' units
+    const int wdcu = rt % DU;
+    int wlrel = 0, wgrel = 0, wllds = 0, whp = HW_;
+    bool wint = false;
+    float wsa[VEC], wsb[VEC];
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) {
+      wsa[q] = 0.f;
+      wsb[q] = 0.f;
+    }
+    if constexpr (WSH) {
+      const int u = DN + rt;
+      int hp = u < D_UNITS ? u / DU : HW_;
+      if constexpr (BSPLIT) {   // halo-ring pixel bp: top row, bottom row, left column, right column
+        const int bp = rt / DU;
+        hp = rt >= D_UNITS - IU ? HW_
+             : bp < RS         ? bp
+             : bp < 2 * RS     ? (TH + 1) * RS + bp - RS
+             : bp < 2 * RS + TH ? (bp - 2 * RS + 1) * RS
+                                : (bp - 2 * RS - TH + 1) * RS + RS - 1;
+      }
+      const int hq = hp < HW_ ? hp : 0;
+      const int hy = hq / RS, hx = hq - hy * RS;
+      whp = hp;
+      wlrel = (hy * W + hx) * (int)d.x_ps + rdn_coff32(d.x_c0 + wdcu * VEC, (int)d.x_ps, (int)d.x_pl);
+      wgrel = (hy * W + hx) * (int)d.gate_ps + rdn_coff32(wdcu * VEC, (int)d.gate_ps, (int)d.gate_pl);
+      wllds = hq * DROW + wdcu * 16;
+      wint = hp < HW_ && hy >= 1 && hy <= TH && hx >= 1 && hx <= TW;
+    }
+    auto loadD = [&](int tt, u32x4& lr, u32x4& gr) {
+      int oy, ox, on;
+      origin(tt, oy, ox, on);
+      const int64_t hpix0 = ((int64_t)on * H + (oy - 1)) * W + (ox - 1);
+      const bool ok = in_img(whp, oy, ox);
+      lr = rdn_ld16(rdn_rsrc(DY + hpix0 * d.x_ps), ok, wlrel * 2);
+      if constexpr (GT) gr = rdn_ld16(rdn_rsrc(PR + hpix0 * d.gate_ps), ok, wgrel * 2);
+      else gr = u32x4{0u, 0u, 0u, 0u};
+    };
+    auto storeD = [&](const u32x4& lr, const u32x4& gr, bool live, int doff) {
+      unsigned char* const dst = whp < HW_ ? dyh + doff + wllds : dump + rt * 16;
+      if constexpr (!GT) {
+        *(u32x4*)dst = lr;
+      } else {
+        const f32x4 a0 = *(const f32x4*)(alds + wdcu * VEC), a1 = *(const f32x4*)(alds + wdcu * VEC + 4);
+        if (BSPLIT || !live) {   // (block-uniform) the packed gate, no partials
+          u32x4 o;
+          o[0] = rdn_gate2(lr[0], gr[0], a0[0], a0[1]);
+          o[1] = rdn_gate2(lr[1], gr[1], a0[2], a0[3]);
+          o[2] = rdn_gate2(lr[2], gr[2], a1[0], a1[1]);
+          o[3] = rdn_gate2(lr[3], gr[3], a1[2], a1[3]);
+          *(u32x4*)dst = o;
+          return;
+        }
+        float dy[VEC], pr[VEC];
+        Unit16<bf16>::unpack(lr, dy);
+        Unit16<bf16>::unpack(gr, pr);
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) {
+          const bool pos = pr[q] > 0.f;
+          if (wint && !pos) wsa[q] += pr[q] * dy[q];
+          dy[q] = pos ? dy[q] : (q < 4 ? a0[q] : a1[q - 4]) * dy[q];
+          if (wint) wsb[q] += dy[q];
+        }
+        *(u32x4*)dst = Unit16<bf16>::pack(dy);
+      }
     };
     // lane (g, q = r>>2, pp = r&3) supplies pixels {4g+q, 16+4g+q} of each 32-pixel
     // k-step (tile rows 2ks, 2ks+1) and channels / columns 4pp..4pp+3
@@ -797,11 +919,14 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     // the shapes whose budget held them, spilled once both parities were unrolled)
     // and a run-time parity (unrolled, the two copies spilled the 64 / 80-column ones)
     {
-      u32x4 lA[X_IT];
+      u32x4 lA[X_IT], dl = {0u, 0u, 0u, 0u}, dg = {0u, 0u, 0u, 0u};
       if (t < t_hi) {
         load(t, lA);
+        if constexpr (WSH) loadD(t, dl, dg);
         store(lA, 0);
+        if constexpr (WSH) storeD(dl, dg, half == 0, 0);
         load(min(t + per, t_last), lA);
+        if constexpr (WSH) loadD(min(t + per, t_last), dl, dg);
       }
       __syncthreads();   // weights + first halos
       for (int k = 0; t < t_hi; ++k) {
@@ -810,10 +935,12 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
         const unsigned long long s0 = DW_NOW();
 #endif
         store(lA, (cur ^ 1) * Cfg::X_BYTES);   // tile t + per (a re-read past the range)
+        if constexpr (WSH) storeD(dl, dg, half == 0 && t + per < t_hi, (cur ^ 1) * Cfg::D_BYTES);
 #ifdef DW_STAMPS
         const unsigned long long s1 = DW_NOW();
 #endif
         load(min(t + 2 * per, t_last), lA);
+        if constexpr (WSH) loadD(min(t + 2 * per, t_last), dl, dg);
 #ifdef DW_STAMPS
         const unsigned long long s2 = DW_NOW();
 #endif
@@ -909,6 +1036,15 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
           if (m < wg.mdim) ws[(int64_t)m * ncol_all + col] = accW[i][j][e];
         }
     }
+    if constexpr (WSH) {   // (the loop's last barrier freed the halo area, as for the D waves)
+      if (GT && wg.part) {
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+          red[(NR + rt) * VEC + k] = wsa[k];
+          red[RED_T * VEC + (NR + rt) * VEC + k] = wsb[k];
+        }
+      }
+    }
   }
 
   // dalpha / dbias partials of this split, fixed order.  Both roles arrive at this
@@ -920,9 +1056,9 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       constexpr int DUC = CK / VEC;
       const int cg = rt / VEC, k = rt % VEC;
       float a = 0.f, b = 0.f;
-      for (int rr = 0; rr < NR / DUC; ++rr) {
+      for (int rr = 0; rr < RED_T / DUC; ++rr) {   // D threads, then (WSH) W threads
         a += red[(rr * DUC + cg) * VEC + k];
-        b += red[NR * VEC + (rr * DUC + cg) * VEC + k];
+        b += red[RED_T * VEC + (rr * DUC + cg) * VEC + k];
       }
       if (rt < wg.mdim) {
         wg.part[((int64_t)slab * 2 + 0) * wg.mdim + rt] = a;   // (zero rows in half 1)
