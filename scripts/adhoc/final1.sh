@@ -1,0 +1,3 @@
+cd $GRAFT_REPO_ROOT; export TMPDIR=/tmp; O=gpurun_out/r05_final1; mkdir -p $O
+timeout -k 10 700 python -u -m pytest tests/ -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || exit $?
+timeout -k 10 400 python -u bench.py --layer-report $O/layers.json > $O/bench.json 2> $O/bench.err || exit $?
