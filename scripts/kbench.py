@@ -39,6 +39,9 @@ SHAPES = [
     ("L0 dgrad3 32->80", 16, 256, 256, 32, 32, 80, "dgrad"),
     ("L1 conv_3 160->64", 16, 128, 128, 160, 160, 64, "fwd"),
     ("L1 dgrad3 64->160", 16, 128, 128, 64, 64, 160, "dgrad"),
+    ("L2 conv_0 128->64", 16, 64, 64, 320, 128, 64, "fwd"),
+    ("L2 conv_2 256->64", 16, 64, 64, 320, 256, 64, "fwd"),
+    ("L2 conv_0 128->64 B32", 32, 64, 64, 320, 128, 64, "fwd"),
     ("L2 conv_3 320->128", 16, 64, 64, 320, 320, 128, "fwd"),
     ("L2 dgrad3 128->320", 16, 64, 64, 128, 128, 320, "dgrad"),
     ("L3 conv_3 640->256", 16, 32, 32, 640, 640, 256, "fwd"),
