@@ -114,8 +114,13 @@ __device__ __forceinline__ void dense_conv(const unsigned char* __restrict__ lds
     const int off = ((tap / 3) * RW + tap % 3) * CP + ci * 2;
     const u32x4 a = WREG ? wreg[j] : *(const u32x4*)(wimg + r * WC::PITCH + g * 16 + j * 64);
     u32x4 b[MTW];
+#ifdef DN_DIAG_NO_LDS   // diagnostic build (timing only): opaque B fragments, no LDS reads
+#pragma unroll
+    for (int i = 0; i < MTW; ++i) asm volatile("" : "=v"(b[i]) : "v"(off));
+#else
 #pragma unroll
     for (int i = 0; i < MTW; ++i) b[i] = *(const u32x4*)(lds + pbase[i] + off);
+#endif
 #ifdef DN_DIAG_NO_MFMA
 #pragma unroll
     for (int i = 0; i < MTW; ++i) { asm volatile("" ::"v"(a), "v"(b[i])); }
@@ -254,7 +259,9 @@ __global__ __launch_bounds__(NT, 1) void conv3_dense_kernel(rdn_dense3_desc d, i
     const int nxt = t + per;
     const int tx = t % tiles_x, t1 = t / tiles_x;
     const int y0 = (t1 % tiles_y) * TH, x0 = tx * TW, nimg = t1 / tiles_y;
+#ifndef DN_DIAG_NO_XLOAD   // diagnostic build (timing only): every tile computes on the first tile's x
     if (nxt < t_hi) load_x(nxt);   // in flight during this tile
+#endif
     const int64_t pix0 = ((int64_t)nimg * H + y0) * W + x0;
     Out o[3];
 #pragma unroll
@@ -267,13 +274,17 @@ __global__ __launch_bounds__(NT, 1) void conv3_dense_kernel(rdn_dense3_desc d, i
       dense_conv<G, 32, 2, G::NMT0, true>(lds, wave, r, g, w0, nullptr, acc);
       dense_epi<G, 2, G::NMT0, 0>(lds, wave, r, g, acc, bias[0], alpha[0], o[0], y0, x0, H, W);
     }
+#ifndef DN_DIAG_NO_BAR
     bar_lds();
+#endif
     {
       f32x4 acc[G::NMT1 / NW];   // (8 x 16: 12 m-tiles padded to 16, the critical path either way)
       dense_conv<G, 48, 1, G::NMT1, true>(lds, wave, r, g, w1, nullptr, acc);
       dense_epi<G, 1, G::NMT1, 1>(lds, wave, r, g, acc, bias[1], alpha[1], o[1], y0, x0, H, W);
     }
+#ifndef DN_DIAG_NO_BAR
     bar_lds();
+#endif
     {
       f32x4 acc[G::NMT2 / NW];
       dense_conv<G, 64, 0, G::NMT2, false>(lds, wave, r, g, nullptr, lds + W2_OFF, acc);
@@ -281,10 +292,12 @@ __global__ __launch_bounds__(NT, 1) void conv3_dense_kernel(rdn_dense3_desc d, i
     }
     bar_lds();   // C's x rows are free (the compiler's own vmcnt wait before store_x
                  // counts the epilogue stores issued after the x loads)
+#ifndef DN_DIAG_NO_XLOAD
     if (nxt < t_hi) {
       store_x();
       bar_lds();
     }
+#endif
     t = nxt;
   }
 }
