@@ -102,7 +102,35 @@ constexpr int NT = 512;   // 8 waves
 #ifndef DW_W16
 #define DW_W16 1     // dX epilogue in 16-byte units (lane-row swap); 0: 8-byte units (A/B)
 #endif
+#ifndef DW_DDMA
+// 1: the pre-gated 64-channel dY halo (the five-part level-1 conv_3) reaches LDS by
+// LDS-DMA (global_load_lds_dwordx4): no VGPR staging, no ds_write pass in the D waves.
+// Dense 128-B pixel rows; physical 16-B unit pu of halo column hx holds logical unit
+// pu ^ (hx & 7) (an exhaustive model of the ds_read_b128 / ds_read_b64_tr_b16 lane
+// groups: both fragment reads conflict-free, as with the padded rows).  Per launch
+// (scripts/dw_kbench.py, profiles/r05_ddma_kbench_ab.txt) 112.0 -> 105.8 us at B16,
+// 210.0 -> 197.2 at B32; the step even within noise
+#define DW_DDMA 1
+#endif
 constexpr int LDS_MAX = 160 * 1024;
+
+__device__ __attribute__((aligned(64))) unsigned int g_dw_zero[16];
+
+template <int N>
+__device__ __forceinline__ void dw_wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+// one LDS-DMA wave-instruction: 16 B per lane from `src` to LDS byte dst + lane*16 (dst
+// wave-uniform, in M0; inline asm, so the compiler does not count it on its waits --
+// the step's explicit vmcnt wait before the barrier is the ordering, as in conv3_big)
+__device__ __forceinline__ void dw_glds16(const void* src, unsigned dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(__builtin_amdgcn_readfirstlane(dst))
+               : "memory");
+}
+__device__ __forceinline__ unsigned dw_lds_addr(const unsigned char* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) unsigned char*)p;
+}
 
 #ifdef DW_STAMPS
 // diagnostic build: per wave, cycles (s_memtime) spent in each phase of the tile loop,
@@ -111,15 +139,18 @@ __device__ unsigned long long g_dw_st[512 * 8 * 8];
 #define DW_NOW() __builtin_amdgcn_s_memtime()
 #endif
 
-template <int BN, int CK, bool GO = false>
+template <int BN, int CK, bool GO = false, bool DDMA_ = false>
 struct DwCfg {
   static constexpr int KC = (9 * CK + 63) / 64 * 64;   // packed dgrad K (rdn_pack_weights, conv3_ws)
   static constexpr int NSTEP = KC / 32;
   static constexpr int WROW = KC * 2 + 32;              // = 32 mod 128: conflict-free B reads
   static constexpr int W_BYTES = BN * WROW;
-  static constexpr int DROW = c3::HaloRow<CK * 2>::V;   // dY halo row stride (b128 and tr16 conflict-free)
+  static constexpr bool DDMA = DDMA_;                   // (DW_DDMA) dense swizzled rows, 1-KB DMA pieces
+  static_assert(!DDMA || (CK == 64 && !GO), "LDS-DMA dY halo: 8 units per pixel row");
+  static constexpr int DROW = DDMA ? CK * 2 : c3::HaloRow<CK * 2>::V;   // dY halo row stride (b128 and tr16 conflict-free)
   static constexpr int XROW = c3::HaloRow<BN * 2>::V;   // X halo row stride
-  static constexpr int D_BYTES = (HW_ * DROW + 15) / 16 * 16;
+  static constexpr int D_PIECES = (HW_ * CK * 2 + 1023) / 1024;
+  static constexpr int D_BYTES = DDMA ? D_PIECES * 1024 : (HW_ * DROW + 15) / 16 * 16;
   static constexpr int X_BYTES = (HW_ * XROW + 15) / 16 * 16;
   static constexpr int CT_BYTES = 0;                    // dX leaves from the accumulators
   static constexpr bool SB_ = DW_SB && !((BN == 64 && CK == 16) || (BN == 32 && CK == 32));
@@ -129,6 +160,7 @@ struct DwCfg {
   // with it (64->32 34.1 -> 35.6, h2 46.8 / 52.9 -> 47.7 / 54.4, go 46.5 -> 48.9) and h5
   // even: off there
   static constexpr bool WSH = DW_WSHARE && SB_ && (CK == 16 || BN == 80 || (GO && BN == 48));
+  static_assert(!DDMA || (SB_ && !WSH), "LDS-DMA dY halo: the one-barrier schedule, D waves only");
   static constexpr int RED_BYTES = 2 * (WSH ? 512 : 256) * 8 * 4;   // dalpha/dbias partial reduction (aliases)
   static constexpr int AL_BYTES = (CK * 4 + 15) / 16 * 16;   // gate slopes
   static constexpr int GAL_BYTES = GO ? BN * 4 : 0;           // gate-out: the finished layer's slopes
@@ -161,7 +193,8 @@ struct DwCfg {
 template <int BN, int CK, int NH, bool GO, bool GT>
 __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wgrad_desc wg, int tiles_x, int tiles_y,
                                                          int ntiles) {
-  using Cfg = DwCfg<BN, CK, GO>;
+  using Cfg = DwCfg<BN, CK, GO, DW_DDMA && !GT && CK == 64 && !GO>;
+  constexpr bool DDMA = Cfg::DDMA;
   constexpr int VEC = 8;
   constexpr int KC = Cfg::KC, NSTEP = Cfg::NSTEP, WROW = Cfg::WROW, DROW = Cfg::DROW, XROW = Cfg::XROW;
   constexpr int NR = 256;                               // threads per role
@@ -288,6 +321,33 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       llds[it] = hq * DROW + dcu * 16;
       if (hp < HW_ && hy >= 1 && hy <= TH && hx >= 1 && hx <= TW) dint |= 1u << it;
     }
+    // (DDMA) dY halo piece pc = rw + 4 j (1 KB): halo bytes pc * 1024 + lane * 16 ->
+    // pixel hp, physical unit pu = lane & 7 holding logical unit pu ^ (hx & 7);
+    // out-of-image pixels (and the pad past the halo) read the zero line
+    constexpr int DPW = DDMA ? (Cfg::D_PIECES + 3) / 4 : 1;
+    int prel[DPW], php[DPW];
+#pragma unroll
+    for (int j = 0; j < DPW; ++j) {
+      const int hp = (rw + 4 * j) * 8 + (lane >> 3);
+      const int hq = hp < HW_ ? hp : 0;
+      const int hy = hq / RS, hx = hq - hy * RS;
+      php[j] = hp;
+      prel[j] = (hy * W + hx) * (int)d.x_ps +
+                rdn_coff32(d.x_c0 + ((lane & 7) ^ (hx & 7)) * VEC, (int)d.x_ps, (int)d.x_pl);
+    }
+    auto issue_d = [&](int tt, int doff) {
+      int oy, ox, on;
+      origin(tt, oy, ox, on);
+      const bf16* const db = DY + (((int64_t)on * H + (oy - 1)) * W + (ox - 1)) * d.x_ps;
+      const unsigned dst = dw_lds_addr(dyh) + doff;
+#pragma unroll
+      for (int j = 0; j < DPW; ++j) {
+        const int pc = rw + 4 * j;
+        if (pc >= Cfg::D_PIECES) break;   // wave-uniform
+        const void* src = in_img(php[j], oy, ox) ? (const void*)(db + prel[j]) : (const void*)g_dw_zero;
+        dw_glds16(src, dst + pc * 1024);
+      }
+    };
     float sa[VEC], sb[VEC];
 #pragma unroll
     for (int q = 0; q < VEC; ++q) {
@@ -441,7 +501,15 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
         offA[j] = a_lane + ((tap / 3) * RS + tap % 3) * DROW + ci * 2;
       }
     }
-    const unsigned char* const pda = dyh + (KALIGN ? a_lane + g * 16 : 0);
+    const unsigned char* const pda = dyh + (DDMA ? (2 * rw * RS + r) * DROW : KALIGN ? a_lane + g * 16 : 0);
+    // (DDMA) in-row byte offset of the lane's unit ci / 8 + g at halo column r + dx
+    int dsw[DDMA ? 3 : 1][DDMA ? 2 : 1];
+    if constexpr (DDMA) {
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) dsw[dx][c] = dx * DROW + (((4 * c + g) ^ ((r + dx) & 7)) * 16);
+    }
     const unsigned char* const pdb = wl + r * WROW + g * 16;
     auto dgrad_tile = [&](int tt, const u32x2 (&eo)[MT][NE], int doff) {
       f32x4 acc[MT][NTL];
@@ -467,7 +535,10 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       constexpr bool GP_LATE = DW_GP_LATE == 1 || (DW_GP_LATE < 0 && BN == 64 && NH == 1);
       if constexpr (GO && !GP_LATE) load_gp();
       auto aoff_of = [&](int j) {
-        if constexpr (KALIGN) {
+        if constexpr (DDMA) {
+          const int k0 = 32 * j, tap = k0 / CK, ci = k0 - tap * CK;
+          return (tap / 3) * RS * DROW + dsw[tap % 3][ci / 32];
+        } else if constexpr (KALIGN) {
           const int k0 = 32 * j;
           int tap = k0 / CK;
           const int ci = k0 - tap * CK;
@@ -599,16 +670,31 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     // tile, and the gate pass overlaps the W waves' MFMAs instead of idling them (two
     // register sets in flight measured no faster and spill the 80-column shape)
     if (t < t_hi) {
-      load(t, lA, gA);
-      store(lA, gA, half == 0, 0);
-      load(min(t + per, t_last), lA, gA);
-      load_epi(t, eC);   // (after the halo, as in the loop: the loop head's vmcnt waits then
-                         // count the same ops on entry and on the back edge, not vmcnt(0))
+      if constexpr (DDMA) {
+        issue_d(t, 0);
+        load_epi(t, eC);
+        dw_wait_vm<0>();
+      } else {
+        load(t, lA, gA);
+        store(lA, gA, half == 0, 0);
+        load(min(t + per, t_last), lA, gA);
+        load_epi(t, eC);   // (after the halo, as in the loop: the loop head's vmcnt waits then
+                           // count the same ops on entry and on the back edge, not vmcnt(0))
+      }
     }
     __syncthreads();   // weights + first halos
     auto step = [&](u32x4 (&lc)[D_ITD], u32x4 (&gc)[D_ITD], const u32x2 (&ec)[MT][NE], u32x2 (&en)[MT][NE],
                     int cur) -> bool {
       const int t1 = t + per;
+      if constexpr (DDMA) {   // tile t1's dY halo DMA'd into buffer cur^1 during this tile's MFMAs
+        load_epi(min(t1, t_last), en);
+        issue_d(min(t1, t_last), (cur ^ 1) * Cfg::D_BYTES);
+        dgrad_tile(t, ec, cur * Cfg::D_BYTES);   // MFMAs + dX stores
+        dw_wait_vm<W16 ? NTL : MT * NTL>();       // the DMA done (this tile's dX stores may fly)
+        __syncthreads();   // buffer cur consumed, buffer cur^1 written
+        t = t1;
+        return t < t_hi;
+      }
 #ifdef DW_STAMPS
       const unsigned long long s0 = DW_NOW();
 #endif
@@ -822,7 +908,13 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     // lane (g, q = r>>2, pp = r&3) supplies pixels {4g+q, 16+4g+q} of each 32-pixel
     // k-step (tile rows 2ks, 2ks+1) and channels / columns 4pp..4pp+3
     const int q4 = r >> 2, pp = r & 3;
-    const unsigned char* const pwa = dyh + (RS + 4 * g + q4 + 1) * DROW + 4 * pp * 2;   // interior (0, 4g+q)
+    const unsigned char* const pwa = dyh + (RS + 4 * g + q4 + 1) * DROW + (DDMA ? 0 : 4 * pp * 2);   // interior (0, 4g+q)
+    // in-row byte offset of m-tile i's channels 16 i + 4 pp .. +3 (DDMA: the unit of halo
+    // column 4g+q+1 swizzled)
+    int wsw[MTW];
+#pragma unroll
+    for (int i = 0; i < MTW; ++i)
+      wsw[i] = DDMA ? (((2 * i + (pp >> 1)) ^ ((4 * g + q4 + 1) & 7)) * 16 + (pp & 1) * 8) : i * 32;
     const unsigned char* const pwb = xh + (4 * g + q4) * XROW;
     auto boff = [&](int j) {   // column offset of n-tile rw + 4 j (recomputed: registers)
       const int nt = rw + 4 * j;
@@ -846,9 +938,9 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
 #pragma unroll
         for (int i = 0; i < MTW; ++i) {
           const i16x4 lo =
-              __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, pwa + doff + (2 * ks) * RS * DROW + i * 32));
+              __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, pwa + doff + (2 * ks) * RS * DROW + wsw[i]));
           const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              RDN_LDS_PTR(i16x4, pwa + doff + (2 * ks + 1) * RS * DROW + i * 32));
+              RDN_LDS_PTR(i16x4, pwa + doff + (2 * ks + 1) * RS * DROW + wsw[i]));
           a[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
         }
       };
@@ -888,9 +980,9 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
 #pragma unroll
         for (int i = 0; i < MTW; ++i) {
           const i16x4 lo =
-              __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, pwa + doff + (2 * ks) * RS * DROW + i * 32));
+              __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, pwa + doff + (2 * ks) * RS * DROW + wsw[i]));
           const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              RDN_LDS_PTR(i16x4, pwa + doff + (2 * ks + 1) * RS * DROW + i * 32));
+              RDN_LDS_PTR(i16x4, pwa + doff + (2 * ks + 1) * RS * DROW + wsw[i]));
           af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
         }
 #pragma unroll
@@ -1200,7 +1292,7 @@ bool dw_serves(const rdn_conv_desc* d, const rdn_wgrad_desc* wg) {
 
 template <int BN, int CK, int NH = 1, bool GO = false, bool GT = true>
 int launch_dw(const rdn_conv_desc* d, const rdn_wgrad_desc* wg, hipStream_t st) {
-  if constexpr (!DwCfg<BN, CK, GO>::FITS) {
+  if constexpr (!DwCfg<BN, CK, GO, DW_DDMA && !GT && CK == 64 && !GO>::FITS) {
     return 1;
   } else {
     const int tiles_x = d->w / TW, tiles_y = d->h / TH;
