@@ -91,7 +91,8 @@ constexpr int NT = 512;   // 8 waves
 #define DW_GP_LATE 0
 #endif
 #ifndef DW_DPF
-#define DW_DPF 0     // dgrad: next k-step's fragments read before the current MFMAs (A/B)
+#define DW_DPF 0     // dgrad: next k-step's fragments read before the current MFMAs (A/B; re-measured
+                     // after the h5 dY DMA: no shape faster, <64,32,go> spills, r05_xdma_dpf_kbench)
 #endif
 #ifndef DW_WSHARE
 // 1: on the one-barrier (SB) shapes the W waves load and gate the last partial round
@@ -111,6 +112,14 @@ constexpr int NT = 512;   // 8 waves
 // (scripts/dw_kbench.py, profiles/r05_ddma_kbench_ab.txt) 112.0 -> 105.8 us at B16,
 // 210.0 -> 197.2 at B32; the step even within noise
 #define DW_DDMA 1
+#endif
+#ifndef DW_XDMA
+// 1: with DW_DDMA, the 32-column X halo of the W waves by LDS-DMA as well (dense 64-B
+// rows, physical unit p of halo column x holds logical unit p ^ (((x >> 2) & 1) << 1):
+// the ds_read_b64_tr_b16 B reads conflict-free by exhaustive model).  Measured even to
+// slower (h5 94.4 -> 95.1 us at B16, 204.8 -> 206.7 at B32, profiles/r05_xdma_dpf_kbench.txt):
+// the W waves' X staging is not on the tile's critical path; off
+#define DW_XDMA 0
 #endif
 constexpr int LDS_MAX = 160 * 1024;
 
@@ -148,10 +157,12 @@ struct DwCfg {
   static constexpr bool DDMA = DDMA_;                   // (DW_DDMA) dense swizzled rows, 1-KB DMA pieces
   static_assert(!DDMA || (CK == 64 && !GO), "LDS-DMA dY halo: 8 units per pixel row");
   static constexpr int DROW = DDMA ? CK * 2 : c3::HaloRow<CK * 2>::V;   // dY halo row stride (b128 and tr16 conflict-free)
-  static constexpr int XROW = c3::HaloRow<BN * 2>::V;   // X halo row stride
+  static constexpr bool XDMA = DW_XDMA && DDMA && BN == 32;
+  static constexpr int XROW = XDMA ? BN * 2 : c3::HaloRow<BN * 2>::V;   // X halo row stride
   static constexpr int D_PIECES = (HW_ * CK * 2 + 1023) / 1024;
   static constexpr int D_BYTES = DDMA ? D_PIECES * 1024 : (HW_ * DROW + 15) / 16 * 16;
-  static constexpr int X_BYTES = (HW_ * XROW + 15) / 16 * 16;
+  static constexpr int X_PIECES = (HW_ * BN * 2 + 1023) / 1024;
+  static constexpr int X_BYTES = XDMA ? X_PIECES * 1024 : (HW_ * XROW + 15) / 16 * 16;
   static constexpr int CT_BYTES = 0;                    // dX leaves from the accumulators
   static constexpr bool SB_ = DW_SB && !((BN == 64 && CK == 16) || (BN == 32 && CK == 32));
   // W waves gate the dY halo ring (BSPLIT below) on the level-0 shapes: per launch at B16
@@ -920,7 +931,37 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       const int nt = rw + 4 * j;
       const int c = nt < NT_ALL ? nt * 16 + 4 * pp : 0;
       const int tp = c / BN, ci = c - (c / BN) * BN;
+      if constexpr (Cfg::XDMA) {   // the unit of halo column 4g+q+tp%3 swizzled
+        const int x = 4 * g + q4 + tp % 3;
+        return ((tp / 3) * RS + tp % 3) * XROW + (((ci >> 3) ^ (((x >> 2) & 1) << 1)) << 4) + (ci & 7) * 2;
+      }
       return ((tp / 3) * RS + tp % 3) * XROW + ci * 2;
+    };
+    // (XDMA) X halo piece pc = rw + 4 j (1 KB): halo bytes pc * 1024 + lane * 16 -> pixel
+    // hp, physical unit lane & 3 holding logical unit (lane & 3) ^ (((hx >> 2) & 1) << 1)
+    constexpr int XPW = Cfg::XDMA ? (Cfg::X_PIECES + 3) / 4 : 1;
+    int xprel[XPW], xphp[XPW];
+#pragma unroll
+    for (int j = 0; j < XPW; ++j) {
+      const int hp = (rw + 4 * j) * 16 + (lane >> 2);
+      const int hq = hp < HW_ ? hp : 0;
+      const int hy = hq / RS, hx = hq - hy * RS;
+      xphp[j] = hp;
+      xprel[j] = (hy * W + hx) * (int)wg.b_ps +
+                 rdn_coff32(xc0 + ((lane & 3) ^ (((hx >> 2) & 1) << 1)) * VEC, (int)wg.b_ps, (int)wg.b_pl);
+    }
+    auto issue_x = [&](int tt, int xoff) {
+      int oy, ox, on;
+      origin(tt, oy, ox, on);
+      const bf16* const xb = XS + (((int64_t)on * H + (oy - 1)) * W + (ox - 1)) * wg.b_ps;
+      const unsigned dst = dw_lds_addr(xh) + xoff;
+#pragma unroll
+      for (int j = 0; j < XPW; ++j) {
+        const int pc = rw + 4 * j;
+        if (pc >= Cfg::X_PIECES) break;   // wave-uniform
+        const void* src = in_img(xphp[j], oy, ox) ? (const void*)(xb + xprel[j]) : (const void*)g_dw_zero;
+        dw_glds16(src, dst + pc * 1024);
+      }
     };
     f32x4 accW[MTW][NTW];
 #pragma unroll
@@ -1012,6 +1053,21 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     // and a run-time parity (unrolled, the two copies spilled the 64 / 80-column ones)
     {
       u32x4 lA[X_IT], dl = {0u, 0u, 0u, 0u}, dg = {0u, 0u, 0u, 0u};
+      if constexpr (Cfg::XDMA) {   // tile t + per's X halo DMA'd into buffer cur^1 during this tile's MFMAs
+        if (t < t_hi) {
+          issue_x(t, 0);
+          dw_wait_vm<0>();
+        }
+        __syncthreads();   // weights + first halos
+        for (int k = 0; t < t_hi; ++k) {
+          const int cur = k & 1;
+          issue_x(min(t + per, t_last), (cur ^ 1) * Cfg::X_BYTES);
+          wgrad_tile(cur * Cfg::X_BYTES, cur * Cfg::D_BYTES);
+          dw_wait_vm<0>();
+          __syncthreads();   // buffers cur consumed, buffers cur^1 written
+          t += per;
+        }
+      } else {
       if (t < t_hi) {
         load(t, lA);
         if constexpr (WSH) loadD(t, dl, dg);
@@ -1046,6 +1102,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
         st[0] += s1 - s0; st[1] += s2 - s1; st[2] += s3 - s2; st[4] += s4 - s3; st[6] += 1;
 #endif
         t += per;
+      }
       }
     }
     } else {
