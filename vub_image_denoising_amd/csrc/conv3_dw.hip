@@ -113,6 +113,14 @@ constexpr int NT = 512;   // 8 waves
 // 210.0 -> 197.2 at B32; the step even within noise
 #define DW_DDMA 1
 #endif
+#ifndef DW_WREG
+// 1: with DW_DDMA, h5's D waves hold the whole 32-column dgrad weight panel in VGPRs
+// (18 k-steps x 2 n-tiles x 16 B = 144 registers per lane) instead of LDS: their
+// fragment reads per MFMA halve (the dY operand only), and the panel leaves the LDS
+// (240 VGPRs, no scratch, 86 KB of LDS).  Per launch (profiles/r05_wreg_kbench_ab.txt)
+// 106.8 -> 99.0 us at B16, 202.8 -> 185.3 at B32; step +0.3 / +0.2 % (interleaved)
+#define DW_WREG 1
+#endif
 #ifndef DW_XDMA
 // 1: with DW_DDMA, the 32-column X halo of the W waves by LDS-DMA as well (dense 64-B
 // rows, physical unit p of halo column x holds logical unit p ^ (((x >> 2) & 1) << 1):
@@ -153,8 +161,9 @@ struct DwCfg {
   static constexpr int KC = (9 * CK + 63) / 64 * 64;   // packed dgrad K (rdn_pack_weights, conv3_ws)
   static constexpr int NSTEP = KC / 32;
   static constexpr int WROW = KC * 2 + 32;              // = 32 mod 128: conflict-free B reads
-  static constexpr int W_BYTES = BN * WROW;
   static constexpr bool DDMA = DDMA_;                   // (DW_DDMA) dense swizzled rows, 1-KB DMA pieces
+  static constexpr bool WREG = DW_WREG && DDMA && BN == 32;   // (DW_WREG) dgrad weights in VGPRs
+  static constexpr int W_BYTES = WREG ? 0 : BN * WROW;
   static_assert(!DDMA || (CK == 64 && !GO), "LDS-DMA dY halo: 8 units per pixel row");
   static constexpr int DROW = DDMA ? CK * 2 : c3::HaloRow<CK * 2>::V;   // dY halo row stride (b128 and tr16 conflict-free)
   static constexpr bool XDMA = DW_XDMA && DDMA && BN == 32;
@@ -281,7 +290,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
   {
     const bf16* __restrict__ WP = (const bf16*)d.wp;
     constexpr int UPRW = KC / VEC;
-    for (int u = tid; u < BN * UPRW; u += NT) {
+    for (int u = tid; u < (Cfg::WREG ? 0 : BN * UPRW); u += NT) {
       const int n = u / UPRW, k8 = u - n * UPRW;
       *(u32x4*)(wl + n * WROW + k8 * 16) = *(const u32x4*)(WP + (int64_t)(col0 + n) * d.kp + k8 * VEC);
     }
@@ -522,6 +531,16 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
         for (int c = 0; c < 2; ++c) dsw[dx][c] = dx * DROW + (((4 * c + g) ^ ((r + dx) & 7)) * 16);
     }
     const unsigned char* const pdb = wl + r * WROW + g * 16;
+    // (WREG) the lane's B fragments of every k-step: weight row col0 + 16 jn + r, k 32 j + 8 g
+    u32x4 wreg[Cfg::WREG ? NSTEP : 1][Cfg::WREG ? NTL : 1];
+    if constexpr (Cfg::WREG) {
+      const bf16* __restrict__ WP = (const bf16*)d.wp;
+#pragma unroll
+      for (int j = 0; j < NSTEP; ++j)
+#pragma unroll
+        for (int jn = 0; jn < NTL; ++jn)
+          wreg[j][jn] = *(const u32x4*)(WP + (int64_t)(col0 + jn * 16 + r) * d.kp + j * 32 + g * 8);
+    }
     auto dgrad_tile = [&](int tt, const u32x2 (&eo)[MT][NE], int doff) {
       f32x4 acc[MT][NTL];
 #pragma unroll
@@ -584,7 +603,8 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
 #pragma unroll
         for (int i = 0; i < MT; ++i) fa[i] = *(const u32x4*)(pda + doff + ao + i * RS * DROW);
 #pragma unroll
-        for (int jn = 0; jn < NTL; ++jn) fb[jn] = *(const u32x4*)(pdb + jn * 16 * WROW + j * 64);
+        for (int jn = 0; jn < NTL; ++jn)
+          fb[jn] = Cfg::WREG ? wreg[Cfg::WREG ? j : 0][Cfg::WREG ? jn : 0] : *(const u32x4*)(pdb + jn * 16 * WROW + j * 64);
 #endif
 #pragma unroll
         for (int i = 0; i < MT; ++i)
