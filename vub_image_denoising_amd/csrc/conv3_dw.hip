@@ -121,6 +121,12 @@ constexpr int NT = 512;   // 8 waves
 // 106.8 -> 99.0 us at B16, 202.8 -> 185.3 at B32; step +0.3 / +0.2 % (interleaved)
 #define DW_WREG 1
 #endif
+#ifndef DW_WREG_ALL
+// A/B: the resident register panel on every non-gate-out shape it fits (<= 144 registers):
+// within the bench's noise on the level-0/1 shapes, three of them spill
+// (profiles/r05_wreg_all_kbench.txt) -- their D waves are not LDS-read bound; off
+#define DW_WREG_ALL 0
+#endif
 #ifndef DW_XDMA
 // 1: with DW_DDMA, the 32-column X halo of the W waves by LDS-DMA as well (dense 64-B
 // rows, physical unit p of halo column x holds logical unit p ^ (((x >> 2) & 1) << 1):
@@ -162,7 +168,8 @@ struct DwCfg {
   static constexpr int NSTEP = KC / 32;
   static constexpr int WROW = KC * 2 + 32;              // = 32 mod 128: conflict-free B reads
   static constexpr bool DDMA = DDMA_;                   // (DW_DDMA) dense swizzled rows, 1-KB DMA pieces
-  static constexpr bool WREG = DW_WREG && DDMA && BN == 32;   // (DW_WREG) dgrad weights in VGPRs
+  static constexpr int WREGS = (KC / 32) * (BN / 16) * 4;     // panel registers per D lane
+  static constexpr bool WREG = DW_WREG && !GO && ((DDMA && BN == 32) || (DW_WREG_ALL && WREGS <= 144));
   static constexpr int W_BYTES = WREG ? 0 : BN * WROW;
   static_assert(!DDMA || (CK == 64 && !GO), "LDS-DMA dY halo: 8 units per pixel row");
   static constexpr int DROW = DDMA ? CK * 2 : c3::HaloRow<CK * 2>::V;   // dY halo row stride (b128 and tr16 conflict-free)
