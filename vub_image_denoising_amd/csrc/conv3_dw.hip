@@ -593,7 +593,8 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
 #pragma unroll
         for (int i = 0; i < MT; ++i) pa_[b][i] = *(const u32x4*)(pda + doff + ao + i * RS * DROW);
 #pragma unroll
-        for (int jn = 0; jn < NTL; ++jn) pb_[b][jn] = *(const u32x4*)(pdb + jn * 16 * WROW + j * 64);
+        for (int jn = 0; jn < NTL; ++jn)
+          pb_[b][jn] = Cfg::WREG ? wreg[Cfg::WREG ? j : 0][Cfg::WREG ? jn : 0] : *(const u32x4*)(pdb + jn * 16 * WROW + j * 64);
       };
       rdf(0, 0);
 #endif
