@@ -326,6 +326,31 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     return (hp < HW_) & ((unsigned)(oy - 1 + hy) < (unsigned)H) & ((unsigned)(ox - 1 + hx) < (unsigned)W);
   };
 
+  // (DW_XDMA == 2) the X halo of tile tt by LDS-DMA, pieces wv, wv + 4, ... (issued by the
+  // D waves, which wait at the barrier while the W waves' wgrad is the tile's critical path)
+  auto issue_x_d = [&](int tt, int xoff, int wv) {
+    if constexpr (Cfg::XDMA) {
+      int oy, ox, on;
+      origin(tt, oy, ox, on);
+      const bf16* const xb = XS + (((int64_t)on * H + (oy - 1)) * W + (ox - 1)) * wg.b_ps;
+      const unsigned dst = dw_lds_addr(dyh + Cfg::DB * Cfg::D_BYTES) + xoff;
+      const int xc0 = wg.b_c0 + col0;
+#pragma unroll
+      for (int j = 0; j < (Cfg::X_PIECES + 3) / 4; ++j) {
+        const int pc = wv + 4 * j;
+        if (pc >= Cfg::X_PIECES) break;   // wave-uniform
+        const int hp = pc * 16 + (lane >> 2);
+        const int hq = hp < HW_ ? hp : 0;
+        const int hy = hq / RS, hx = hq - hy * RS;
+        const int rel = (hy * W + hx) * (int)wg.b_ps +
+                        rdn_coff32(xc0 + ((lane & 3) ^ (((hx >> 2) & 1) << 1)) * VEC, (int)wg.b_ps, (int)wg.b_pl);
+        const void* src = in_img(hp, oy, ox) ? (const void*)(xb + rel) : (const void*)g_dw_zero;
+        dw_glds16(src, dst + pc * 1024);
+      }
+    }
+  };
+  constexpr bool XBYD = Cfg::XDMA && DW_XDMA == 2;
+
   // The two roles run separate loops (their loop-carried registers do not overlap)
   // with the same barriers per tile.  At the top of a step LDS holds tile t and the
   // register set `cur` holds tile t + per in flight; the step issues t + 2 per into
@@ -711,6 +736,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     if (t < t_hi) {
       if constexpr (DDMA) {
         issue_d(t, 0);
+        if constexpr (XBYD) issue_x_d(t, 0, rw);
         load_epi(t, eC);
         dw_wait_vm<0>();
       } else {
@@ -726,11 +752,25 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
                     int cur) -> bool {
       const int t1 = t + per;
       if constexpr (DDMA) {   // tile t1's dY halo DMA'd into buffer cur^1 during this tile's MFMAs
+#ifdef DW_STAMPS
+        const unsigned long long s0 = DW_NOW();
+#endif
         load_epi(min(t1, t_last), en);
         issue_d(min(t1, t_last), (cur ^ 1) * Cfg::D_BYTES);
+        if constexpr (XBYD) issue_x_d(min(t1, t_last), (cur ^ 1) * Cfg::X_BYTES, rw);
+#ifdef DW_STAMPS
+        const unsigned long long s1 = DW_NOW();
+#endif
         dgrad_tile(t, ec, cur * Cfg::D_BYTES);   // MFMAs + dX stores
+#ifdef DW_STAMPS
+        const unsigned long long s4 = DW_NOW();
+#endif
         dw_wait_vm<W16 ? NTL : MT * NTL>();       // the DMA done (this tile's dX stores may fly)
         __syncthreads();   // buffer cur consumed, buffer cur^1 written
+#ifdef DW_STAMPS
+        const unsigned long long s5 = DW_NOW();
+        st[1] += s1 - s0; st[2] += st_mid - s1; st[3] += s4 - st_mid; st[4] += s5 - s4; st[6] += 1;
+#endif
         t = t1;
         return t < t_hi;
       }
@@ -1082,17 +1122,30 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     {
       u32x4 lA[X_IT], dl = {0u, 0u, 0u, 0u}, dg = {0u, 0u, 0u, 0u};
       if constexpr (Cfg::XDMA) {   // tile t + per's X halo DMA'd into buffer cur^1 during this tile's MFMAs
-        if (t < t_hi) {
+        if (t < t_hi && !XBYD) {
           issue_x(t, 0);
           dw_wait_vm<0>();
         }
         __syncthreads();   // weights + first halos
         for (int k = 0; t < t_hi; ++k) {
           const int cur = k & 1;
-          issue_x(min(t + per, t_last), (cur ^ 1) * Cfg::X_BYTES);
+#ifdef DW_STAMPS
+          const unsigned long long s0 = DW_NOW();
+#endif
+          if constexpr (!XBYD) issue_x(min(t + per, t_last), (cur ^ 1) * Cfg::X_BYTES);
+#ifdef DW_STAMPS
+          const unsigned long long s2 = DW_NOW();
+#endif
           wgrad_tile(cur * Cfg::X_BYTES, cur * Cfg::D_BYTES);
-          dw_wait_vm<0>();
+#ifdef DW_STAMPS
+          const unsigned long long s3 = DW_NOW();
+#endif
+          if constexpr (!XBYD) dw_wait_vm<0>();
           __syncthreads();   // buffers cur consumed, buffers cur^1 written
+#ifdef DW_STAMPS
+          const unsigned long long s4 = DW_NOW();
+          st[1] += s2 - s0; st[2] += s3 - s2; st[4] += s4 - s3; st[6] += 1;
+#endif
           t += per;
         }
       } else {
