@@ -127,6 +127,15 @@ constexpr int NT = 512;   // 8 waves
 // (profiles/r05_wreg_all_kbench.txt) -- their D waves are not LDS-read bound; off
 #define DW_WREG_ALL 0
 #endif
+#ifndef DW_WREG_SYNC
+#define DW_WREG_SYNC 0   // A/B: the register panel's loads waited for before the tile loop (below)
+#endif
+#ifndef DW_D3
+// 1: with the register panel (h5), THREE dY halo buffers: each D wave issues the DMA of
+// tile t + 2 per after its dX epilogue, so a DMA has a whole step to land (stamps: with
+// two buffers the D waves waited ~830 cycles per tile for the DMA issued that step)
+#define DW_D3 0
+#endif
 #ifndef DW_XDMA
 // 1: with DW_DDMA, the 32-column X halo of the W waves by LDS-DMA as well (dense 64-B
 // rows, physical unit p of halo column x holds logical unit p ^ (((x >> 2) & 1) << 1):
@@ -175,7 +184,8 @@ struct DwCfg {
   static constexpr int DROW = DDMA ? CK * 2 : c3::HaloRow<CK * 2>::V;   // dY halo row stride (b128 and tr16 conflict-free)
   static constexpr bool XDMA = DW_XDMA && DDMA && BN == 32;
   static constexpr int XROW = XDMA ? BN * 2 : c3::HaloRow<BN * 2>::V;   // X halo row stride
-  static constexpr int D_PIECES = (HW_ * CK * 2 + 1023) / 1024;
+  static constexpr bool D3 = DW_D3 && WREG;
+  static constexpr int D_PIECES = D3 ? ((HW_ * CK * 2 + 1023) / 1024 + 3) / 4 * 4 : (HW_ * CK * 2 + 1023) / 1024;
   static constexpr int D_BYTES = DDMA ? D_PIECES * 1024 : (HW_ * DROW + 15) / 16 * 16;
   static constexpr int X_PIECES = (HW_ * BN * 2 + 1023) / 1024;
   static constexpr int X_BYTES = XDMA ? X_PIECES * 1024 : (HW_ * XROW + 15) / 16 * 16;
@@ -202,7 +212,7 @@ struct DwCfg {
   // 32->16 59 -> 54 us, 80->32 135 -> 133, 64->32 36 -> 34; the 64->16 and 32->32
   // shapes ran 1-3 us slower and keep two barriers per tile)
   static constexpr bool SB = SB_;
-  static constexpr int DB = SB ? 2 : 1;
+  static constexpr int DB = D3 ? 3 : SB ? 2 : 1;
   static constexpr int BASE = W_BYTES + DB * D_BYTES + CT_BYTES + AL_BYTES + GAL_BYTES;
   // X halo buffers in LDS: 2 for the LDS double buffer, 1 where it would not fit
   // (96 columns were tried: <96,32> spills 128 B in the W loop, so they stay on the
@@ -572,6 +582,15 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
 #pragma unroll
         for (int jn = 0; jn < NTL; ++jn)
           wreg[j][jn] = *(const u32x4*)(WP + (int64_t)(col0 + jn * 16 + r) * d.kp + j * 32 + g * 8);
+      // consumed here, before the tile loop: otherwise hipcc counts these loads as pending
+      // at the loop's first MFMAs and its vmcnt waits there (down to vmcnt(2)) also drain
+      // the halo DMA and epilogue loads in flight on every later tile
+#if DW_WREG_SYNC
+#pragma unroll
+      for (int j = 0; j < NSTEP; ++j)
+#pragma unroll
+        for (int jn = 0; jn < NTL; ++jn) asm volatile("" : "+v"(wreg[j][jn]));
+#endif
     }
     auto dgrad_tile = [&](int tt, const u32x2 (&eo)[MT][NE], int doff) {
       f32x4 acc[MT][NTL];
@@ -736,6 +755,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     if (t < t_hi) {
       if constexpr (DDMA) {
         issue_d(t, 0);
+        if constexpr (Cfg::D3) issue_d(min(t + per, t_last), Cfg::D_BYTES);
         if constexpr (XBYD) issue_x_d(t, 0, rw);
         load_epi(t, eC);
         dw_wait_vm<0>();
@@ -748,9 +768,21 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       }
     }
     __syncthreads();   // weights + first halos
+    int dsel = 0;   // (D3) the dY buffer of tile t
     auto step = [&](u32x4 (&lc)[D_ITD], u32x4 (&gc)[D_ITD], const u32x2 (&ec)[MT][NE], u32x2 (&en)[MT][NE],
                     int cur) -> bool {
       const int t1 = t + per;
+      if constexpr (Cfg::D3) {   // tile t + 2 per's dY halo DMA'd after this tile's epilogue
+        constexpr int NST = W16 ? NTL : MT * NTL;   // epilogue loads = dX stores per lane
+        load_epi(min(t1, t_last), en);
+        dgrad_tile(t, ec, dsel * Cfg::D_BYTES);
+        issue_d(min(t + 2 * per, t_last), (dsel == 0 ? 2 : dsel - 1) * Cfg::D_BYTES);
+        dw_wait_vm<2 * NST + Cfg::D_PIECES / 4>();   // tile t1's DMA (issued one step ago) done
+        __syncthreads();
+        dsel = dsel == 2 ? 0 : dsel + 1;
+        t = t1;
+        return t < t_hi;
+      }
       if constexpr (DDMA) {   // tile t1's dY halo DMA'd into buffer cur^1 during this tile's MFMAs
 #ifdef DW_STAMPS
         const unsigned long long s0 = DW_NOW();
@@ -1136,7 +1168,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
 #ifdef DW_STAMPS
           const unsigned long long s2 = DW_NOW();
 #endif
-          wgrad_tile(cur * Cfg::X_BYTES, cur * Cfg::D_BYTES);
+          wgrad_tile(cur * Cfg::X_BYTES, (Cfg::D3 ? k % 3 : cur) * Cfg::D_BYTES);
 #ifdef DW_STAMPS
           const unsigned long long s3 = DW_NOW();
 #endif
@@ -1173,7 +1205,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
 #ifdef DW_STAMPS
         const unsigned long long s2 = DW_NOW();
 #endif
-        wgrad_tile(cur * Cfg::X_BYTES, cur * Cfg::D_BYTES);
+        wgrad_tile(cur * Cfg::X_BYTES, (Cfg::D3 ? k % 3 : cur) * Cfg::D_BYTES);
 #ifdef DW_STAMPS
         const unsigned long long s3 = DW_NOW();
 #endif
