@@ -770,14 +770,16 @@ def main():
         _log(f"rank {rank}: graph capture failed ({e.__cause__!r})")
     if world > 1 and graph and not all_ranks_ok(capture_err is None):
         # the hipGraph capture of the data-parallel step raised on some rank: no rank may
-        # replay alone.  Under this bench's own launcher every rank exits and the job
-        # restarts eagerly from fresh processes; under an external launcher (torchrun)
-        # every rank drops to eager steps together
-        if own_launcher:
-            dist.destroy_process_group()
-            sys.exit(EXIT_GRAPH_FAILED)
-        _log(f"rank {rank}: a rank's capture failed; every rank runs the step eagerly")
-        tr.graph = None
+        # replay alone, and the RCCL communicator is suspect after a failed capture (a
+        # capture that failed after some collectives were enqueued can leave the ranks'
+        # op counts mismatched, and the first eager all-reduce would hang until the
+        # watchdog).  Every rank exits EXIT_GRAPH_FAILED under every launcher: bench's own
+        # launcher restarts the job eagerly from fresh processes; under torchrun, rerun
+        # with --graph off
+        _log(f"rank {rank}: a rank's capture failed; exiting (rerun with --graph off under an external launcher)"
+             if not own_launcher else f"rank {rank}: a rank's capture failed; the launcher restarts eagerly")
+        dist.destroy_process_group()
+        sys.exit(EXIT_GRAPH_FAILED)
     elif capture_err is not None:
         raise capture_err
     graph = tr.graph is not None

@@ -152,7 +152,16 @@ def _rccl_worker(init_file, q):
                 raise AssertionError(f"losses differ: eager {le.item()} graph {lg.item()} nosync {ln.item()}")
         torch.cuda.synchronize()
         fE, fG, fN = (m.unet._rdn_flat.flat for m in (mE, mG, mN))
-        res = (bool(torch.equal(fE, fG)), bool(torch.equal(fG, fN)), nb, gG.graph_nodes)
+        # exposure figure (advisor r05): with no bucket launched during a backward, every
+        # all-reduce runs after the backward's end, so the exposed time must be > 0 (the
+        # round-5 form recorded its end event at the launch, not the completion: ~0)
+        gs = GradSync(mE.unet._rdn_flat, bucket_mb=0.05)
+        gs.timing = []
+        for _ in range(3):
+            gs.begin()
+            gs.finish()
+        exposed = gs.exposed_ms()
+        res = (bool(torch.equal(fE, fG)), bool(torch.equal(fG, fN)), nb, gG.graph_nodes, exposed)
         dist.destroy_process_group()
         q.put(res)
     except Exception as e:  # report instead of hanging the parent on q.get
@@ -173,8 +182,10 @@ def test_rccl_world1_graph_captured_gradsync(tmp_path):
         if p.is_alive():
             p.kill()
     assert not isinstance(res, str), res
-    same_eager, same_nosync, nb, nodes = res
-    print(f"RCCL world 1: {nb} buckets, graph nodes {nodes}; replay == eager: {same_eager}, == no-sync: {same_nosync}")
+    same_eager, same_nosync, nb, nodes, exposed = res
+    print(f"RCCL world 1: {nb} buckets, graph nodes {nodes}; replay == eager: {same_eager}, == no-sync: {same_nosync}; "
+          f"unhidden all-reduce {exposed} ms")
     assert nb > 1
+    assert exposed is not None and exposed > 0.0
     assert same_eager and same_nosync
     assert p.exitcode == 0

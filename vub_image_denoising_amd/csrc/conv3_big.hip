@@ -41,19 +41,11 @@ namespace {
 
 __device__ __attribute__((aligned(64))) unsigned int g_big_zero[16];
 
-#ifndef BIG_W16
-// 1 (round 5): pairs of pixel rows exchanged between lane rows g, g^1 (v_permlane16_swap)
+// Round 5: pairs of pixel rows are exchanged between lane rows g, g^1 (v_permlane16_swap)
 // so the epilogue moves 16-byte units (8 channels of one pixel) instead of 8-byte ones:
-// half the epilogue memory instructions (as conv3_dw's dX epilogue)
-#define BIG_W16 1
-#endif
-
-#ifndef BIG_PF
-// 1: the next k-step's fragments are read before the current MFMAs (two fragment sets
-// live; bit-identical).  Round 4, interleaved on one box: B16 +0.6 %, B32 +0.5 %
-// (profiles/r04_v5_big_pf_gate_out_ab.txt)
-#define BIG_PF 1
-#endif
+// half the epilogue memory instructions (as conv3_dw's dX epilogue), except gate-out.
+// Round 4: the next k-step's fragments are read before the current MFMAs (two fragment
+// sets live; bit-identical; B16 +0.6 %, B32 +0.5 %, profiles/r04_v5_big_pf_gate_out_ab.txt).
 
 template <int N>
 __device__ __forceinline__ void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
@@ -147,7 +139,7 @@ __global__ __launch_bounds__(64 * NW, 2) void conv3_big_kernel(rdn_conv_desc d, 
   constexpr bool RES = EP == EP_FWD_RES || EP == EP_RES;
   constexpr bool ACC = EP == EP_ACC;
   constexpr bool GOK = GO && !FWD;   // gate-out epilogue (input gradients only)
-  constexpr bool W16 = BIG_W16 && !GOK && MT % 2 == 0;   // (launch_pt checks the 8-channel alignment)
+  constexpr bool W16 = !GOK && MT % 2 == 0;   // (launch_pt checks the 8-channel alignment)
   static_assert(Cfg::OK, "conv3_big geometry");
 
   __shared__ __attribute__((aligned(1024))) unsigned char lds[Cfg::LDS];
@@ -372,19 +364,14 @@ __global__ __launch_bounds__(64 * NW, 2) void conv3_big_kernel(rdn_conv_desc d, 
   // ROLL: the rolling prefetch where the full second fragment set spilled, the 128-column
   // 64-channel-chunk residual-forward and gate-out items (12-36 B/lane at 255 VGPRs,
   // round 4; without any prefetch they run 4-7 % longer, profiles/r05_spill_*)
-#ifdef BIG_PF_ALL   // variant build for A/B: the round-4 rule (prefetch everywhere)
-  constexpr bool ROLL = false;
-#else
-  constexpr bool ROLL = BIG_PF && BN == 128 && CK == 64 && (GOK || EP == EP_FWD_RES);
-#endif
+  constexpr bool ROLL = BN == 128 && CK == 64 && (GOK || EP == EP_FWD_RES);
   // (the gate-out residual form, which the train step does not launch, spills even so:
   // no prefetch there)
   constexpr bool NOPF = BN == 128 && CK == 64 && GOK && EP == EP_RES;
   auto compute = [&](int jj, const unsigned char* ph, const unsigned char* pbs) {
     if constexpr (NOPF) compute_np(jj, ph, pbs);
     else if constexpr (ROLL) compute_roll(jj, ph, pbs);
-    else if constexpr (BIG_PF) compute_pf(jj, ph, pbs);
-    else compute_np(jj, ph, pbs);
+    else compute_pf(jj, ph, pbs);
   };
 
   // ---- epilogue: straight from the accumulators, through buffer descriptors on the
@@ -720,7 +707,7 @@ int launch_pt(const rdn_conv_desc* d, hipStream_t st, int tiles_x, int tiles_y, 
     return 1;
   } else {
     constexpr bool FWD_ = EP == EP_FWD || EP == EP_FWD_RES;
-    if constexpr (BIG_W16 && !(GO && !FWD_) && Cfg::MT % 2 == 0) {
+    if constexpr (!(GO && !FWD_) && Cfg::MT % 2 == 0) {
       // 16-byte epilogue units: 8-channel aligned operands
       auto a8 = [](int64_t ps, int64_t c0, const void* p) { return ps % 8 == 0 && c0 % 8 == 0 && !((uintptr_t)p & 15); };
       if (!a8(d->out_ps, d->out_c0, d->out)) return 1;
@@ -794,11 +781,7 @@ bool big_ck32_multi() {
 bool big_nw4() {
   static const bool on = [] {
     const char* e = getenv("RDN_BIG_NW4");
-#ifdef BIG_NW4_OFF   // variant build for in-process A/B (scripts/kbench.py)
-    return e && e[0] == '1';
-#else
     return !(e && e[0] == '0');
-#endif
   }();
   return on;
 }

@@ -76,74 +76,21 @@ using c3::TH;
 using c3::TW;
 
 constexpr int NT = 512;   // 8 waves
-#ifndef DW_WPIPE
-#define DW_WPIPE 3   // weight-gradient fragment prefetch depth (0: one k-step at a time)
-#endif
-#ifndef DW_SB
-#define DW_SB 1      // one barrier per tile (dY and X halos double-buffered in LDS)
-#endif
-#ifndef DW_GP_LATE
-// gate-out: 1 = the finished layer's PReLU input loaded after the dgrad MFMAs (its
-// latency exposed, 16 fewer live registers), 0 (default) = before them; -1 = after them
-// on the 64-column single-part shape only, which spills 12 B/lane the other way -- but
-// runs 4-7 % longer per launch without the spill (level-1 conv_0, B16 / B32 layer
-// reports, profiles/r05_spill_layers.txt): the spill stays
-#define DW_GP_LATE 0
-#endif
-#ifndef DW_DPF
-#define DW_DPF 0     // dgrad: next k-step's fragments read before the current MFMAs (A/B; re-measured
-                     // after the h5 dY DMA: no shape faster, <64,32,go> spills, r05_xdma_dpf_kbench)
-#endif
-#ifndef DW_WSHARE
-// 1: on the one-barrier (SB) shapes the W waves load and gate the last partial round
-// of the dY halo units ([(D_IT - 1) * 256, D_UNITS)), which the D waves did -- the D
-// waves are the critical path of a tile, the W waves waited at its barrier (round 5)
-#define DW_WSHARE 1
-#endif
-#ifndef DW_W16
-#define DW_W16 1     // dX epilogue in 16-byte units (lane-row swap); 0: 8-byte units (A/B)
-#endif
-#ifndef DW_DDMA
-// 1: the pre-gated 64-channel dY halo (the five-part level-1 conv_3) reaches LDS by
-// LDS-DMA (global_load_lds_dwordx4): no VGPR staging, no ds_write pass in the D waves.
-// Dense 128-B pixel rows; physical 16-B unit pu of halo column hx holds logical unit
-// pu ^ (hx & 7) (an exhaustive model of the ds_read_b128 / ds_read_b64_tr_b16 lane
-// groups: both fragment reads conflict-free, as with the padded rows).  Per launch
-// (scripts/dw_kbench.py, profiles/r05_ddma_kbench_ab.txt) 112.0 -> 105.8 us at B16,
-// 210.0 -> 197.2 at B32; the step even within noise
-#define DW_DDMA 1
-#endif
-#ifndef DW_WREG
-// 1: with DW_DDMA, h5's D waves hold the whole 32-column dgrad weight panel in VGPRs
-// (18 k-steps x 2 n-tiles x 16 B = 144 registers per lane) instead of LDS: their
-// fragment reads per MFMA halve (the dY operand only), and the panel leaves the LDS
-// (240 VGPRs, no scratch, 86 KB of LDS).  Per launch (profiles/r05_wreg_kbench_ab.txt)
-// 106.8 -> 99.0 us at B16, 202.8 -> 185.3 at B32; step +0.3 / +0.2 % (interleaved)
-#define DW_WREG 1
-#endif
-#ifndef DW_WREG_ALL
-// A/B: the resident register panel on every non-gate-out shape it fits (<= 144 registers):
-// within the bench's noise on the level-0/1 shapes, three of them spill
-// (profiles/r05_wreg_all_kbench.txt) -- their D waves are not LDS-read bound; off
-#define DW_WREG_ALL 0
-#endif
-#ifndef DW_WREG_SYNC
-#define DW_WREG_SYNC 0   // A/B: the register panel's loads waited for before the tile loop (below)
-#endif
-#ifndef DW_D3
-// 1: with the register panel (h5), THREE dY halo buffers: each D wave issues the DMA of
-// tile t + 2 per after its dX epilogue, so a DMA has a whole step to land (stamps: with
-// two buffers the D waves waited ~830 cycles per tile for the DMA issued that step)
-#define DW_D3 0
-#endif
-#ifndef DW_XDMA
-// 1: with DW_DDMA, the 32-column X halo of the W waves by LDS-DMA as well (dense 64-B
-// rows, physical unit p of halo column x holds logical unit p ^ (((x >> 2) & 1) << 1):
-// the ds_read_b64_tr_b16 B reads conflict-free by exhaustive model).  Measured even to
-// slower (h5 94.4 -> 95.1 us at B16, 204.8 -> 206.7 at B32, profiles/r05_xdma_dpf_kbench.txt):
-// the W waves' X staging is not on the tile's critical path; off
-#define DW_XDMA 0
-#endif
+// Schedule (each choice measured per launch and on the step; DESIGN.md sections 9-10):
+//  * weight-gradient fragments prefetched 3 (k-step, n-tile) steps ahead;
+//  * one barrier per tile (dY and X halos double-buffered in LDS) where it measured faster;
+//  * on the level-0 one-barrier shapes the W waves load and gate the dY halo ring and the
+//    D waves the tile interior (the D waves are the critical path of a tile);
+//  * dX epilogue in 16-byte units (lane-row swap by v_permlane16_swap) except gate-out;
+//  * the pre-gated 64-channel dY halo of the five-part level-1 conv_3 (h5) arrives by
+//    LDS-DMA (dense 128-B pixel rows; physical 16-B unit pu of halo column hx holds logical
+//    unit pu ^ (hx & 7): both fragment reads conflict-free by exhaustive model), into THREE
+//    buffers (the DMA of tile t + 2 per issued after tile t's epilogue, so it has a whole
+//    step to land), and h5's D waves hold the whole 32-column dgrad weight panel in VGPRs
+//    (144 registers per lane), waited for before the tile loop.
+//    Per launch at B16 / B32 (profiles/r05_ddma_kbench_ab.txt, r05_wreg_kbench_ab.txt,
+//    r05_h5_d3_kbench.txt): 112.0 -> 105.8 -> 99.0 -> 92.8 us / 210 -> 197 -> 185 -> 189 us.
+constexpr int DW_WPIPE = 3;   // weight-gradient fragment prefetch depth
 constexpr int LDS_MAX = 160 * 1024;
 
 __device__ __attribute__((aligned(64))) unsigned int g_dw_zero[16];
@@ -176,27 +123,27 @@ struct DwCfg {
   static constexpr int KC = (9 * CK + 63) / 64 * 64;   // packed dgrad K (rdn_pack_weights, conv3_ws)
   static constexpr int NSTEP = KC / 32;
   static constexpr int WROW = KC * 2 + 32;              // = 32 mod 128: conflict-free B reads
-  static constexpr bool DDMA = DDMA_;                   // (DW_DDMA) dense swizzled rows, 1-KB DMA pieces
+  static constexpr bool DDMA = DDMA_;                   // dense swizzled rows, 1-KB DMA pieces
   static constexpr int WREGS = (KC / 32) * (BN / 16) * 4;     // panel registers per D lane
-  static constexpr bool WREG = DW_WREG && !GO && ((DDMA && BN == 32) || (DW_WREG_ALL && WREGS <= 144));
+  // the register panel on h5 only: on the other shapes it measured within noise (their D
+  // waves are bound by the load path, not LDS reads) and three spilled
+  static constexpr bool WREG = !GO && DDMA && BN == 32;
   static constexpr int W_BYTES = WREG ? 0 : BN * WROW;
   static_assert(!DDMA || (CK == 64 && !GO), "LDS-DMA dY halo: 8 units per pixel row");
   static constexpr int DROW = DDMA ? CK * 2 : c3::HaloRow<CK * 2>::V;   // dY halo row stride (b128 and tr16 conflict-free)
-  static constexpr bool XDMA = DW_XDMA && DDMA && BN == 32;
-  static constexpr int XROW = XDMA ? BN * 2 : c3::HaloRow<BN * 2>::V;   // X halo row stride
-  static constexpr bool D3 = DW_D3 && WREG;
+  static constexpr int XROW = c3::HaloRow<BN * 2>::V;   // X halo row stride
+  static constexpr bool D3 = WREG;                      // three dY halo buffers (h5)
   static constexpr int D_PIECES = D3 ? ((HW_ * CK * 2 + 1023) / 1024 + 3) / 4 * 4 : (HW_ * CK * 2 + 1023) / 1024;
   static constexpr int D_BYTES = DDMA ? D_PIECES * 1024 : (HW_ * DROW + 15) / 16 * 16;
-  static constexpr int X_PIECES = (HW_ * BN * 2 + 1023) / 1024;
-  static constexpr int X_BYTES = XDMA ? X_PIECES * 1024 : (HW_ * XROW + 15) / 16 * 16;
+  static constexpr int X_BYTES = (HW_ * XROW + 15) / 16 * 16;
   static constexpr int CT_BYTES = 0;                    // dX leaves from the accumulators
-  static constexpr bool SB_ = DW_SB && !((BN == 64 && CK == 16) || (BN == 32 && CK == 32));
+  static constexpr bool SB_ = !((BN == 64 && CK == 16) || (BN == 32 && CK == 32));
   // W waves gate the dY halo ring (BSPLIT below) on the level-0 shapes: per launch at B16
   // (scripts/dw_kbench.py, profiles/r05_wsh_kbench_ab.txt) 32->16 57.0 -> 55.0 us, 80->32
   // 136.4 -> 133.5, up_0.conv (h2, go) 243.9 -> 208.5; the level-1 shapes ran 1-2 us slower
   // with it (64->32 34.1 -> 35.6, h2 46.8 / 52.9 -> 47.7 / 54.4, go 46.5 -> 48.9) and h5
   // even: off there
-  static constexpr bool WSH = DW_WSHARE && SB_ && (CK == 16 || BN == 80 || (GO && BN == 48));
+  static constexpr bool WSH = SB_ && (CK == 16 || BN == 80 || (GO && BN == 48));
   static_assert(!DDMA || (SB_ && !WSH), "LDS-DMA dY halo: the one-barrier schedule, D waves only");
   static constexpr int RED_BYTES = 2 * (WSH ? 512 : 256) * 8 * 4;   // dalpha/dbias partial reduction (aliases)
   static constexpr int AL_BYTES = (CK * 4 + 15) / 16 * 16;   // gate slopes
@@ -230,7 +177,7 @@ struct DwCfg {
 template <int BN, int CK, int NH, bool GO, bool GT>
 __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wgrad_desc wg, int tiles_x, int tiles_y,
                                                          int ntiles) {
-  using Cfg = DwCfg<BN, CK, GO, DW_DDMA && !GT && CK == 64 && !GO>;
+  using Cfg = DwCfg<BN, CK, GO, !GT && CK == 64 && !GO>;
   constexpr bool DDMA = Cfg::DDMA;
   constexpr int VEC = 8;
   constexpr int KC = Cfg::KC, NSTEP = Cfg::NSTEP, WROW = Cfg::WROW, DROW = Cfg::DROW, XROW = Cfg::XROW;
@@ -336,31 +283,6 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     return (hp < HW_) & ((unsigned)(oy - 1 + hy) < (unsigned)H) & ((unsigned)(ox - 1 + hx) < (unsigned)W);
   };
 
-  // (DW_XDMA == 2) the X halo of tile tt by LDS-DMA, pieces wv, wv + 4, ... (issued by the
-  // D waves, which wait at the barrier while the W waves' wgrad is the tile's critical path)
-  auto issue_x_d = [&](int tt, int xoff, int wv) {
-    if constexpr (Cfg::XDMA) {
-      int oy, ox, on;
-      origin(tt, oy, ox, on);
-      const bf16* const xb = XS + (((int64_t)on * H + (oy - 1)) * W + (ox - 1)) * wg.b_ps;
-      const unsigned dst = dw_lds_addr(dyh + Cfg::DB * Cfg::D_BYTES) + xoff;
-      const int xc0 = wg.b_c0 + col0;
-#pragma unroll
-      for (int j = 0; j < (Cfg::X_PIECES + 3) / 4; ++j) {
-        const int pc = wv + 4 * j;
-        if (pc >= Cfg::X_PIECES) break;   // wave-uniform
-        const int hp = pc * 16 + (lane >> 2);
-        const int hq = hp < HW_ ? hp : 0;
-        const int hy = hq / RS, hx = hq - hy * RS;
-        const int rel = (hy * W + hx) * (int)wg.b_ps +
-                        rdn_coff32(xc0 + ((lane & 3) ^ (((hx >> 2) & 1) << 1)) * VEC, (int)wg.b_ps, (int)wg.b_pl);
-        const void* src = in_img(hp, oy, ox) ? (const void*)(xb + rel) : (const void*)g_dw_zero;
-        dw_glds16(src, dst + pc * 1024);
-      }
-    }
-  };
-  constexpr bool XBYD = Cfg::XDMA && DW_XDMA == 2;
-
   // The two roles run separate loops (their loop-carried registers do not overlap)
   // with the same barriers per tile.  At the top of a step LDS holds tile t and the
   // register set `cur` holds tile t + per in flight; the step issues t + 2 per into
@@ -430,7 +352,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     // column r): the epilogue operand and dX move as ONE 16-byte load / store per n-tile
     // instead of two 8-byte ones (stamped diagnostic builds: the D waves spent ~1.5k
     // cycles per tile issuing the 8-byte epilogue loads, the critical path of the kernel)
-    constexpr bool W16 = !GO && DW_W16;
+    constexpr bool W16 = !GO;
     int coff_e[NTL], coff_o[NTL], coff_g[NTL];
     bool eok[NTL], gon[NTL];
 #pragma unroll
@@ -461,15 +383,9 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
 #pragma unroll
       for (int it = 0; it < D_ITD; ++it) {
         const bool ok = in_img(uhp[it], oy, ox);
-#ifdef DW_DIAG_NO_LOAD
-        lr[it] = u32x4{(unsigned)ok, 0u, 0u, 0u};
-        gr[it] = u32x4{0u, 0u, 0u, 0u};
-        (void)rd; (void)rg;
-#else
         lr[it] = rdn_ld16(rd, ok, lrel[it] * 2);
         if constexpr (GT) gr[it] = rdn_ld16(rg, ok, grel[it] * 2);
         else gr[it] = u32x4{0u, 0u, 0u, 0u};
-#endif
       }
     };
     // registers -> LDS with the PReLU-backward gate and the dalpha/dbias partials of
@@ -482,12 +398,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
         return;
       }
       const f32x4 a0 = *(const f32x4*)(alds + dcu * VEC), a1 = *(const f32x4*)(alds + dcu * VEC + 4);
-#if !defined(DW_DIAG_NO_GATE) && !defined(DW_SLOW_GATE)
-#ifdef DW_DIAG_FAST_ALL   // diagnostic build: every block gates without counting partials
-      if (true) {
-#else
       if (!live) {   // (block-uniform) no partials to count: the packed gate, ~half the VALU
-#endif
 #pragma unroll
         for (int it = 0; it < D_ITD; ++it) {
           u32x4 o;
@@ -499,7 +410,6 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
         }
         return;
       }
-#endif
 #pragma unroll
       for (int it = 0; it < D_ITD; ++it) {
         float dy[VEC], pr[VEC];
@@ -507,11 +417,6 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
         Unit16<bf16>::unpack(gr[it], pr);
         const bool in = live && ((dint >> it) & 1u);   // a re-read past the range counts nothing
         unsigned char* const dst = uhp[it] < HW_ ? dyh + doff + llds[it] : dump + rt * 16;
-#ifdef DW_DIAG_NO_GATE   // diagnostic build: the raw dY goes to LDS (no gate, no partials)
-        (void)in; (void)a0; (void)a1;
-        *(u32x4*)dst = lr[it];
-        continue;
-#endif
 #pragma unroll
         for (int q = 0; q < VEC; ++q) {
           const bool pos = pr[q] > 0.f;
@@ -530,11 +435,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       if constexpr (W16) {   // one 16-byte unit per n-tile: eo[0][jn] its low, eo[1][jn] its high half
 #pragma unroll
         for (int jn = 0; jn < NTL; ++jn) {
-#if defined(DW_DIAG_NO_LOAD) || defined(DW_DIAG_NO_EPI_LOAD)
-          const u32x4 q = u32x4{(unsigned)eok[jn], 0u, 0u, 0u};
-#else
           const u32x4 q = rdn_ld16(rb, eok[jn], (((2 * rw + (g & 1)) * W + r) * eps + coff_e[jn]) * 2);
-#endif
           eo[0][jn] = u32x2{q[0], q[1]};
           eo[1][jn] = u32x2{q[2], q[3]};
         }
@@ -544,11 +445,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int jn = 0; jn < NTL; ++jn)
-#if defined(DW_DIAG_NO_LOAD) || defined(DW_DIAG_NO_EPI_LOAD)
-          eo[i][jn] = u32x2{(unsigned)eok[jn], 0u};
-#else
           eo[i][jn] = rdn_ld8(rb, eok[jn], (((2 * rw + i) * W + r) * eps + coff_e[jn]) * 2);
-#endif
     };
     // fragments: pixel r of tile rows 2 rw (+1); k-step j covers k = 32 j + 8 g
     const int a_lane = (2 * rw * RS + r) * DROW;
@@ -585,12 +482,10 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       // consumed here, before the tile loop: otherwise hipcc counts these loads as pending
       // at the loop's first MFMAs and its vmcnt waits there (down to vmcnt(2)) also drain
       // the halo DMA and epilogue loads in flight on every later tile
-#if DW_WREG_SYNC
 #pragma unroll
       for (int j = 0; j < NSTEP; ++j)
 #pragma unroll
         for (int jn = 0; jn < NTL; ++jn) asm volatile("" : "+v"(wreg[j][jn]));
-#endif
     }
     auto dgrad_tile = [&](int tt, const u32x2 (&eo)[MT][NE], int doff) {
       f32x4 acc[MT][NTL];
@@ -599,8 +494,9 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
 #pragma unroll
         for (int jn = 0; jn < NTL; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
       // (GO) the finished layer's PReLU input at the gated units, issued before the
-      // MFMAs (prefetched a tile ahead beside `eo` instead: up_0.conv 227 -> 240 us,
-      // the level-1 conv_0 spilled)
+      // MFMAs (prefetched a tile ahead beside `eo` instead: up_0.conv 227 -> 240 us, the
+      // level-1 conv_0 spilled; loaded after the MFMAs: no spill on <64,32,go> but 4-7 %
+      // longer per launch, profiles/r05_spill_layers.txt)
       u32x2 gp[GO ? MT : 1][GO ? NTL : 1];
       auto load_gp = [&]() {
         int oy, ox, on;
@@ -613,8 +509,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
           for (int jn = 0; jn < NTL; ++jn)
             gp[i][jn] = rdn_ld8(rp, gon[jn], (((2 * rw + i) * W + r) * (int)d.gout_pre_ps + coff_g[jn]) * 2);
       };
-      constexpr bool GP_LATE = DW_GP_LATE == 1 || (DW_GP_LATE < 0 && BN == 64 && NH == 1);
-      if constexpr (GO && !GP_LATE) load_gp();
+      if constexpr (GO) load_gp();
       auto aoff_of = [&](int j) {
         if constexpr (DDMA) {
           const int k0 = 32 * j, tap = k0 / CK, ci = k0 - tap * CK;
@@ -629,27 +524,10 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
           return offA[j];
         }
       };
-#if DW_DPF
-      // the next k-step's fragments are read before this one's MFMAs (two sets live)
-      u32x4 pa_[2][MT], pb_[2][NTL];
-      auto rdf = [&](int j, int b) {
-        const int ao = aoff_of(j);
-#pragma unroll
-        for (int i = 0; i < MT; ++i) pa_[b][i] = *(const u32x4*)(pda + doff + ao + i * RS * DROW);
-#pragma unroll
-        for (int jn = 0; jn < NTL; ++jn)
-          pb_[b][jn] = Cfg::WREG ? wreg[Cfg::WREG ? j : 0][Cfg::WREG ? jn : 0] : *(const u32x4*)(pdb + jn * 16 * WROW + j * 64);
-      };
-      rdf(0, 0);
-#endif
+      // (the next k-step's fragments read before the current MFMAs measured no faster on
+      // any shape and spilled <64,32,go>, profiles/r05_xdma_dpf_kbench)
 #pragma unroll
       for (int j = 0; j < NSTEP; ++j) {
-#if DW_DPF
-        if (j + 1 < NSTEP) rdf(j + 1, (j + 1) & 1);
-        __builtin_amdgcn_sched_barrier(0);
-        const u32x4(&fa)[MT] = pa_[j & 1];
-        const u32x4(&fb)[NTL] = pb_[j & 1];
-#else
         const int ao = aoff_of(j);
         u32x4 fa[MT], fb[NTL];
 #pragma unroll
@@ -657,23 +535,17 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
 #pragma unroll
         for (int jn = 0; jn < NTL; ++jn)
           fb[jn] = Cfg::WREG ? wreg[Cfg::WREG ? j : 0][Cfg::WREG ? jn : 0] : *(const u32x4*)(pdb + jn * 16 * WROW + j * 64);
-#endif
 #pragma unroll
         for (int i = 0; i < MT; ++i)
 #pragma unroll
           for (int jn = 0; jn < NTL; ++jn)   // D^T[m = column][n = pixel]
-#ifdef DW_DIAG_NO_MFMA
-            acc[i][jn][0] += __builtin_bit_cast(float, fb[jn][0] ^ fa[i][0]);
-#else
             acc[i][jn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fb[jn]),
                                                                  __builtin_bit_cast(bf16x8, fa[i]), acc[i][jn], 0,
                                                                  0, 0);
-#endif
       }
 #ifdef DW_STAMPS
       st_mid = DW_NOW();
 #endif
-      if constexpr (GO && GP_LATE) load_gp();
       int oy, ox, on;
       origin(tt, oy, ox, on);
       bf16* const ob = (bf16*)d.out + (((int64_t)on * H + oy) * W + ox) * d.out_ps;
@@ -703,9 +575,6 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
             v[4] += bf16lo(eo[1][jn][0]); v[5] += bf16hi(eo[1][jn][0]);
             v[6] += bf16lo(eo[1][jn][1]); v[7] += bf16hi(eo[1][jn][1]);
           }
-#ifdef DW_DIAG_NO_STORE
-          if (flags & (1 << 30))   // never at run time: the values stay live
-#endif
           *(u32x4*)(ob + ((2 * rw + (g & 1)) * W + r) * (int)d.out_ps + coff_o[jn]) = Unit16<bf16>::pack(v);
         }
         return;
@@ -738,9 +607,6 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
               continue;
             }
           }
-#ifdef DW_DIAG_NO_STORE
-          if (flags & (1 << 30))   // never at run time: the values stay live
-#endif
           *(u32x2*)(ob + ((2 * rw + i) * W + r) * (int)d.out_ps + coff_o[jn]) = rdn_pack4(v);
         }
     };
@@ -754,9 +620,9 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     // register sets in flight measured no faster and spill the 80-column shape)
     if (t < t_hi) {
       if constexpr (DDMA) {
+        static_assert(Cfg::D3, "the LDS-DMA dY halo runs three buffers");
         issue_d(t, 0);
-        if constexpr (Cfg::D3) issue_d(min(t + per, t_last), Cfg::D_BYTES);
-        if constexpr (XBYD) issue_x_d(t, 0, rw);
+        issue_d(min(t + per, t_last), Cfg::D_BYTES);
         load_epi(t, eC);
         dw_wait_vm<0>();
       } else {
@@ -772,7 +638,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     auto step = [&](u32x4 (&lc)[D_ITD], u32x4 (&gc)[D_ITD], const u32x2 (&ec)[MT][NE], u32x2 (&en)[MT][NE],
                     int cur) -> bool {
       const int t1 = t + per;
-      if constexpr (Cfg::D3) {   // tile t + 2 per's dY halo DMA'd after this tile's epilogue
+      if constexpr (DDMA) {   // tile t + 2 per's dY halo DMA'd after this tile's epilogue
         constexpr int NST = W16 ? NTL : MT * NTL;   // epilogue loads = dX stores per lane
         load_epi(min(t1, t_last), en);
         dgrad_tile(t, ec, dsel * Cfg::D_BYTES);
@@ -780,29 +646,6 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
         dw_wait_vm<2 * NST + Cfg::D_PIECES / 4>();   // tile t1's DMA (issued one step ago) done
         __syncthreads();
         dsel = dsel == 2 ? 0 : dsel + 1;
-        t = t1;
-        return t < t_hi;
-      }
-      if constexpr (DDMA) {   // tile t1's dY halo DMA'd into buffer cur^1 during this tile's MFMAs
-#ifdef DW_STAMPS
-        const unsigned long long s0 = DW_NOW();
-#endif
-        load_epi(min(t1, t_last), en);
-        issue_d(min(t1, t_last), (cur ^ 1) * Cfg::D_BYTES);
-        if constexpr (XBYD) issue_x_d(min(t1, t_last), (cur ^ 1) * Cfg::X_BYTES, rw);
-#ifdef DW_STAMPS
-        const unsigned long long s1 = DW_NOW();
-#endif
-        dgrad_tile(t, ec, cur * Cfg::D_BYTES);   // MFMAs + dX stores
-#ifdef DW_STAMPS
-        const unsigned long long s4 = DW_NOW();
-#endif
-        dw_wait_vm<W16 ? NTL : MT * NTL>();       // the DMA done (this tile's dX stores may fly)
-        __syncthreads();   // buffer cur consumed, buffer cur^1 written
-#ifdef DW_STAMPS
-        const unsigned long long s5 = DW_NOW();
-        st[1] += s1 - s0; st[2] += st_mid - s1; st[3] += s4 - st_mid; st[4] += s5 - s4; st[6] += 1;
-#endif
         t = t1;
         return t < t_hi;
       }
@@ -832,6 +675,9 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     };
     if (t < t_hi)
       while (step(lA, gA, eC, eN, 0) && step(lA, gA, eN, eC, 1)) {}
+    // the last step issued one more DMA (a re-read of the last tile): it must land before
+    // the block's LDS is released (or, with partials, re-used below)
+    if constexpr (DDMA) dw_wait_vm<0>();
     } else {
     if (t < t_hi) {
       load(t, lA, gA);
@@ -934,11 +780,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
 #pragma unroll
       for (int it = 0; it < X_IT; ++it) {
         const int ll = xlds(it);
-#ifdef DW_DIAG_NO_LOAD
-        lr[it] = u32x4{(unsigned)in_img(ll < 0 ? HW_ : ll / XROW, oy, ox), 0u, 0u, 0u};
-#else
         lr[it] = rdn_ld16(rx, in_img(ll < 0 ? HW_ : ll / XROW, oy, ox), xrel(it) * 2);
-#endif
       }
     };
     auto store = [&](const u32x4 (&lr)[X_IT], int xoff) {
@@ -1031,44 +873,13 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
       const int nt = rw + 4 * j;
       const int c = nt < NT_ALL ? nt * 16 + 4 * pp : 0;
       const int tp = c / BN, ci = c - (c / BN) * BN;
-      if constexpr (Cfg::XDMA) {   // the unit of halo column 4g+q+tp%3 swizzled
-        const int x = 4 * g + q4 + tp % 3;
-        return ((tp / 3) * RS + tp % 3) * XROW + (((ci >> 3) ^ (((x >> 2) & 1) << 1)) << 4) + (ci & 7) * 2;
-      }
       return ((tp / 3) * RS + tp % 3) * XROW + ci * 2;
-    };
-    // (XDMA) X halo piece pc = rw + 4 j (1 KB): halo bytes pc * 1024 + lane * 16 -> pixel
-    // hp, physical unit lane & 3 holding logical unit (lane & 3) ^ (((hx >> 2) & 1) << 1)
-    constexpr int XPW = Cfg::XDMA ? (Cfg::X_PIECES + 3) / 4 : 1;
-    int xprel[XPW], xphp[XPW];
-#pragma unroll
-    for (int j = 0; j < XPW; ++j) {
-      const int hp = (rw + 4 * j) * 16 + (lane >> 2);
-      const int hq = hp < HW_ ? hp : 0;
-      const int hy = hq / RS, hx = hq - hy * RS;
-      xphp[j] = hp;
-      xprel[j] = (hy * W + hx) * (int)wg.b_ps +
-                 rdn_coff32(xc0 + ((lane & 3) ^ (((hx >> 2) & 1) << 1)) * VEC, (int)wg.b_ps, (int)wg.b_pl);
-    }
-    auto issue_x = [&](int tt, int xoff) {
-      int oy, ox, on;
-      origin(tt, oy, ox, on);
-      const bf16* const xb = XS + (((int64_t)on * H + (oy - 1)) * W + (ox - 1)) * wg.b_ps;
-      const unsigned dst = dw_lds_addr(xh) + xoff;
-#pragma unroll
-      for (int j = 0; j < XPW; ++j) {
-        const int pc = rw + 4 * j;
-        if (pc >= Cfg::X_PIECES) break;   // wave-uniform
-        const void* src = in_img(xphp[j], oy, ox) ? (const void*)(xb + xprel[j]) : (const void*)g_dw_zero;
-        dw_glds16(src, dst + pc * 1024);
-      }
     };
     f32x4 accW[MTW][NTW];
 #pragma unroll
     for (int i = 0; i < MTW; ++i)
 #pragma unroll
       for (int j = 0; j < NTW; ++j) accW[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#if DW_WPIPE > 0
     // (k-step, n-tile) steps in one software pipeline: the B fragments of step s + PD
     // are read before step s's MFMAs, the A fragments of k-step ks + 1 at the start of
     // ks (the plain per-k-step form waited on each fragment right after reading it:
@@ -1103,48 +914,10 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
         if (rw + 4 * j < NT_ALL) {   // wave-uniform
 #pragma unroll
           for (int i = 0; i < MTW; ++i)
-#ifdef DW_DIAG_NO_MFMA
-            accW[i][j][0] += __builtin_bit_cast(float, __builtin_bit_cast(u32x4, af[ks & 1][i])[0] ^
-                                                           __builtin_bit_cast(u32x4, bq[st % NQ])[0]);
-#else
             accW[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks & 1][i], bq[st % NQ], accW[i][j], 0, 0, 0);
-#endif
         }
       }
     };
-#else
-    auto wgrad_tile = [&](int xoff, int doff) {
-#pragma unroll
-      for (int ks = 0; ks < TH / 2; ++ks) {
-        __builtin_amdgcn_sched_barrier(0);   // k-steps stay apart: fragment registers of one at a time
-        bf16x8 af[MTW];
-#pragma unroll
-        for (int i = 0; i < MTW; ++i) {
-          const i16x4 lo =
-              __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, pwa + doff + (2 * ks) * RS * DROW + wsw[i]));
-          const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              RDN_LDS_PTR(i16x4, pwa + doff + (2 * ks + 1) * RS * DROW + wsw[i]));
-          af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-        }
-#pragma unroll
-        for (int j = 0; j < NTW; ++j) {
-          if (rw + 4 * j >= NT_ALL) continue;   // wave-uniform
-          const unsigned char* b = pwb + xoff + boff(j) + (2 * ks) * RS * XROW;
-          const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, b));
-          const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, b + RS * XROW));
-          const bf16x8 bfr = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-#pragma unroll
-          for (int i = 0; i < MTW; ++i)
-#ifdef DW_DIAG_NO_MFMA
-            accW[i][j][0] += __builtin_bit_cast(float, __builtin_bit_cast(u32x4, af[i])[0] ^ __builtin_bit_cast(u32x4, bfr)[0]);
-#else
-            accW[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, accW[i][j], 0, 0, 0);
-#endif
-        }
-      }
-    };
-#endif
-
     if constexpr (Cfg::SB) {
     // the D waves' schedule (one barrier per tile): step k computes tile t from X
     // buffer k&1 (and the dY halo buffer k&1) while tile t + per, issued one step
@@ -1153,34 +926,6 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
     // and a run-time parity (unrolled, the two copies spilled the 64 / 80-column ones)
     {
       u32x4 lA[X_IT], dl = {0u, 0u, 0u, 0u}, dg = {0u, 0u, 0u, 0u};
-      if constexpr (Cfg::XDMA) {   // tile t + per's X halo DMA'd into buffer cur^1 during this tile's MFMAs
-        if (t < t_hi && !XBYD) {
-          issue_x(t, 0);
-          dw_wait_vm<0>();
-        }
-        __syncthreads();   // weights + first halos
-        for (int k = 0; t < t_hi; ++k) {
-          const int cur = k & 1;
-#ifdef DW_STAMPS
-          const unsigned long long s0 = DW_NOW();
-#endif
-          if constexpr (!XBYD) issue_x(min(t + per, t_last), (cur ^ 1) * Cfg::X_BYTES);
-#ifdef DW_STAMPS
-          const unsigned long long s2 = DW_NOW();
-#endif
-          wgrad_tile(cur * Cfg::X_BYTES, (Cfg::D3 ? k % 3 : cur) * Cfg::D_BYTES);
-#ifdef DW_STAMPS
-          const unsigned long long s3 = DW_NOW();
-#endif
-          if constexpr (!XBYD) dw_wait_vm<0>();
-          __syncthreads();   // buffers cur consumed, buffers cur^1 written
-#ifdef DW_STAMPS
-          const unsigned long long s4 = DW_NOW();
-          st[1] += s2 - s0; st[2] += s3 - s2; st[4] += s4 - s3; st[6] += 1;
-#endif
-          t += per;
-        }
-      } else {
       if (t < t_hi) {
         load(t, lA);
         if constexpr (WSH) loadD(t, dl, dg);
@@ -1215,7 +960,6 @@ __global__ __launch_bounds__(NT, 1) void conv3_dw_kernel(rdn_conv_desc d, rdn_wg
         st[0] += s1 - s0; st[1] += s2 - s1; st[2] += s3 - s2; st[4] += s4 - s3; st[6] += 1;
 #endif
         t += per;
-      }
       }
     }
     } else {
@@ -1462,7 +1206,7 @@ bool dw_serves(const rdn_conv_desc* d, const rdn_wgrad_desc* wg) {
 
 template <int BN, int CK, int NH = 1, bool GO = false, bool GT = true>
 int launch_dw(const rdn_conv_desc* d, const rdn_wgrad_desc* wg, hipStream_t st) {
-  if constexpr (!DwCfg<BN, CK, GO, DW_DDMA && !GT && CK == 64 && !GO>::FITS) {
+  if constexpr (!DwCfg<BN, CK, GO, !GT && CK == 64 && !GO>::FITS) {
     return 1;
   } else {
     const int tiles_x = d->w / TW, tiles_y = d->h / TH;

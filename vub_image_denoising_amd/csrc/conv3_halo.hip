@@ -495,9 +495,7 @@ int rdn_conv3_chunk_pow2(int cin, int cap) {
 // pixel instead of 3-6 passes of 32 B), else the largest power of two <= 64 (bf16)
 // / 32 (fp32) dividing cin.
 int rdn_conv3_chunk_impl(int cin, int dtype) {
-#ifndef RDN_NO_WIDE_CK
   if (dtype == RDN_BF16 && (cin == 48 || cin == 80 || cin == 96)) return cin;
-#endif
   return rdn_conv3_chunk_pow2(cin, dtype == RDN_BF16 ? 64 : 32);
 }
 

@@ -34,12 +34,8 @@ using c3::TH;
 using c3::TW;
 
 constexpr int LDS_2BLK = 80 * 1024;     // two resident blocks per CU below this
-#ifndef WS_W16
-#define WS_W16 1  // accumulator epilogue in 16-byte units (pixel-row pairs swapped between lane rows)
-#endif
-#ifndef WS_PF
-#define WS_PF 0   // accumulator-epilogue path: k-steps of fragments read ahead of the MFMAs
-#endif
+// accumulator epilogue (<= 64 columns) in 16-byte units (pixel-row pairs swapped between
+// lane rows); fragments read k-step by k-step (reading k-steps ahead measured no gain, r05)
 constexpr int LDS_MAX = 160 * 1024;
 
 template <int BN, int CK>
@@ -291,10 +287,10 @@ __global__ __launch_bounds__(NT, 2) void conv3_ws_kernel(rdn_conv_desc d, int ti
   int ae_co[AE ? NTL : 1], ae_cp[AE ? NTL : 1], ae_ce[AE ? NTL : 1];
   bool ae_eok[AE ? NTL : 1];
   f32x4 ae_b[AE ? NTL : 1], ae_a[AE ? NTL : 1];
-  f32x4 ae_b2[AE && WS_W16 && BN <= 64 ? NTL : 1], ae_a2[AE && WS_W16 && BN <= 64 ? NTL : 1];
+  f32x4 ae_b2[AE && BN <= 64 ? NTL : 1], ae_a2[AE && BN <= 64 ? NTL : 1];
   // (MT == 2: the two pixel rows of a wave pair up; up to 64 columns: the wider
   // instantiations spilled with the second bias / slope registers)
-  constexpr bool W16 = AE && WS_W16 && BN <= 64;
+  constexpr bool W16 = AE && BN <= 64;
   if constexpr (AE) {
 #pragma unroll
     for (int jn = 0; jn < NTL; ++jn) {
@@ -345,9 +341,7 @@ __global__ __launch_bounds__(NT, 2) void conv3_ws_kernel(rdn_conv_desc d, int ti
     for (int i = 0; i < MT; ++i)
 #pragma unroll
       for (int jn = 0; jn < NTL; ++jn) acc[i][jn] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // fragments of k-step j + WS_PF read before the MFMAs of j (a sched barrier keeps
-    // them there: hipcc's own schedule waited on each read one MFMA pair later)
-    constexpr int PF = WS_PF, NB = PF + 1;
+    constexpr int PF = 0, NB = PF + 1;
     u32x4 af[NB][MT], bfr[NB][NTL];
     auto rd = [&](int j, int b) {
       int ao;
@@ -683,7 +677,7 @@ int launch_ws(const rdn_conv_desc* d, hipStream_t st) {
     if (d->gate && NT % HU != 0) return 1;
     // accumulator epilogue: full tiles, NHWC 4-channel groups, 8-byte aligned operands
     const int64_t span = (int64_t)TH * d->w;
-    constexpr bool w16 = WS_W16 && BN <= 64;
+    constexpr bool w16 = BN <= 64;
     auto ok4 = [](int64_t ps, int64_t c0, const void* p) {   // (w16: 16-byte units of 8 channels)
       return w16 ? (ps % 8 == 0 && c0 % 8 == 0 && !((uintptr_t)p & 15)) : (ps % 4 == 0 && c0 % 4 == 0 && !((uintptr_t)p & 7));
     };
@@ -733,9 +727,6 @@ int ws_bn(const rdn_conv_desc* d, hipStream_t st) {
 
 // 0 = launched, < 0 = error, 1 = shape not served here (caller uses conv3_halo)
 int rdn_conv3_ws_launch(const rdn_conv_desc* d, int ck, hipStream_t st) {
-#ifdef RDN_NO_WS
-  return 1;
-#endif
   if (!ws_enabled() || d->dtype != RDN_BF16 || d->bn || ck != d->cin || d->ncols > 96 || d->gout) return 1;
   if (d->x_ps % 8 || d->x_c0 % 8 || ((uintptr_t)d->x & 15) || ((uintptr_t)d->wp & 15) || d->kp % 8) return 1;
   switch (ck) {

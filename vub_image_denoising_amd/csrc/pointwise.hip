@@ -73,12 +73,7 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
-#ifndef RDN_PRELU_MINB
-#define RDN_PRELU_MINB 1
-#endif
-#ifndef RDN_PRELU_PU
-#define RDN_PRELU_PU 4
-#endif
+constexpr int RDN_PRELU_PU = 4;   // pixel iterations per trip of the NHWC fast path
 
 static int grid_for(int64_t n, int per_block, int cap = 8192) {
   int64_t b = (n + per_block - 1) / per_block;
@@ -95,7 +90,7 @@ template <typename T>
 // (<= 64 VGPRs: one wave per SIMD still fits beside a two-wave weight-gradient block of
 // the side stream -- 2 x 218 of 512 -- so the pass is not confined to the CUs the
 // side stream leaves free)
-__global__ __launch_bounds__(256, RDN_PRELU_MINB) void prelu_bwd_kernel(int64_t pixels, int H, int W, int C, int cpad,
+__global__ __launch_bounds__(256, 1) void prelu_bwd_kernel(int64_t pixels, int H, int W, int C, int cpad,
                                                         const T* __restrict__ dy, int64_t dy_ps, int dy_c0,
                                                         int64_t dy_pl, const float* __restrict__ dy_nchw, const T* __restrict__ pre,
                                                         int64_t pre_ps, const float* __restrict__ alpha, T* __restrict__ dyp,
@@ -116,7 +111,6 @@ __global__ __launch_bounds__(256, RDN_PRELU_MINB) void prelu_bwd_kernel(int64_t 
   const int64_t stride = (int64_t)gridDim.x * ppb;
   int64_t p0 = (int64_t)blockIdx.x * ppb + pl;
   const int64_t dy_cf = rdn_coff(dy_c0 + grp * VEC, dy_ps, dy_pl);   // channel offset of this thread's unit
-#ifndef RDN_NO_PRELU_UNROLL
   // NHWC fast path: 4 pixel iterations per trip with all 8 loads issued first
   // (unconditional, from a clamped valid pixel) -- the plain loop exposes one
   // HBM round trip per pixel, which is what the small level-2/3 passes pay
@@ -150,7 +144,6 @@ __global__ __launch_bounds__(256, RDN_PRELU_MINB) void prelu_bwd_kernel(int64_t 
       }
     }
   }
-#endif
   if (active) {
     for (int64_t p = p0; p < pixels; p += stride) {
       float g[VEC], x[VEC], o[VEC];

@@ -49,12 +49,6 @@ constexpr int TH = 8, TW = 16, TP = TH * TW;
 constexpr int HW_ = TW + 2, HP = (TH + 2) * HW_;
 constexpr int LDS_MAX = 160 * 1024;
 
-#ifndef WG_NW4
-#define WG_NW4 0    // 1: the 64 x 64 shape on 4-wave blocks (64 x 144 wave tiles)
-#endif
-#ifndef WG_PIPE
-#define WG_PIPE 0   // B-fragment prefetch depth of the (k-step, n-tile) pipeline; 0: the r03 form
-#endif
 
 template <int BM, int CK>
 struct Geo {
@@ -62,12 +56,13 @@ struct Geo {
   // waits on LDS the other multiplies.  r03: 64 x 64 shapes only (64 x 72 wave tiles,
   // 218 VGPRs, 6-8 % faster per launch, profiles/r03_v10_wgrad_glds_diag.txt); the 80-
   // and 96-column groups spilled there, because every k-step's B fragments (NTW of
-  // them, double-buffered) were read ahead at once.  Round 4: the (k-step, n-tile)
-  // software pipeline below (WG_PIPE > 0) keeps only WG_PIPE + 1 B fragments live, so
-  // every shape fits two waves per SIMD -- bit-identical, but 1-6 % slower per launch
-  // on 5 of the 7 train-step shapes and -0.5 % on the step (profiles/r04_v4_wgrad_pipe_*):
-  // kept as the WG_PIPE=n variant, off
-  static constexpr int NW = ((WG_PIPE > 0 && BM >= 32 && !(BM == 64 && CK == 96)) || (BM == 64 && CK == 64 && !WG_NW4)) ? 8 : 4,
+  // them, double-buffered) were read ahead at once.  Round 4: a (k-step, n-tile)
+  // software pipeline with only a few B fragments live, so every shape fits two waves
+  // per SIMD -- bit-identical, but 1-6 % slower per launch on 5 of the 7 train-step
+  // shapes and -0.5 % on the step (profiles/r04_v4_wgrad_pipe_*).  Round 5: 4-wave
+  // blocks with 64 x 144 AGPR wave tiles for 64 x 64 ran 93 -> 100 us
+  // (profiles/r05_wgrad_agpr_kbench_ab.txt).  Neither kept.
+  static constexpr int NW = (BM == 64 && CK == 64) ? 8 : 4,
                        NTH = 64 * NW;   // (64 x 96: 78 VGPRs of spill at two waves per SIMD)
   static constexpr int NCOL = 9 * CK, NT_ALL = (NCOL + 15) / 16;
   // waves as WMv (along M) x WNv (along the 9*CK columns), the same number of
@@ -237,44 +232,6 @@ __global__ __launch_bounds__((Geo<BM, CK>::NTH), 1) void wgrad3_glds_kernel(rdn_
 #pragma unroll
     for (int j = 0; j < NTW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-#if WG_PIPE > 0
-  // one software pipeline over (k-step ks, n-tile j) steps, the order of the r03 loop
-  // (same MFMA sequence per accumulator: bit-identical): the A fragments of k-step
-  // ks + 1 are read at the start of ks, the B fragment of step s + WG_PIPE before
-  // step s's MFMAs (conv3_dw's weight-gradient role does the same)
-  auto compute = [&](int stage) {
-    const unsigned char* const st = lds + stage * G_::STAGE;
-    constexpr int KS = TP / 32, NS = KS * NTW, PD = WG_PIPE, NQ = PD + 1;
-    auto rdA = [&](int ks, bf16x8 (&a)[MTW]) {
-#pragma unroll
-      for (int i = 0; i < MTW; ++i) {
-        const unsigned char* p = st + aoff[i] + ks * 32 * RA;
-        const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, p));
-        const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, p + 16 * RA));
-        a[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-      }
-    };
-    auto rdB = [&](int s) {
-      const unsigned char* p = st + boff[s % NTW] + (s / NTW) * 2 * HW_ * RB;
-      const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, p));
-      const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(RDN_LDS_PTR(i16x4, p + HW_ * RB));
-      return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-    };
-    bf16x8 af[2][MTW], bq[NQ];
-    rdA(0, af[0]);
-#pragma unroll
-    for (int q = 0; q < PD && q < NS; ++q) bq[q] = rdB(q);
-#pragma unroll
-    for (int s = 0; s < NS; ++s) {
-      const int ks = s / NTW, j = s % NTW;
-      if (j == 0 && ks + 1 < KS) rdA(ks + 1, af[(ks + 1) & 1]);
-      if (s + PD < NS) bq[(s + PD) % NQ] = rdB(s + PD);
-#pragma unroll
-      for (int i = 0; i < MTW; ++i)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks & 1][i], bq[s % NQ], acc[i][j], 0, 0, 0);
-    }
-  };
-#else
   auto compute = [&](int stage) {
     const unsigned char* const st = lds + stage * G_::STAGE;
     // all fragments of k-step ks+1 are read before the MFMAs of ks (at one wave per
@@ -326,7 +283,6 @@ __global__ __launch_bounds__((Geo<BM, CK>::NTH), 1) void wgrad3_glds_kernel(rdn_
 #endif
     }
   };
-#endif
 
   // ---- NS-deep ring: up to NS-1 tiles in flight while tile it is multiplied;
   // unrolled by NS so that every stage offset is a constant

@@ -554,7 +554,6 @@ Plan plan(const rdn_wgrad_desc* d) {
   while (ck > cap) ck >>= 1;
   p.ck = ck;
   p.rows = 0;
-#ifndef RDN_NO_WROWS
   if (d->dtype == RDN_BF16) {
     // rows kernel: the widest channel group whose accumulators fit (BM x 9 CK per block)
     // accumulator budget BM x CK <= 2560: two blocks per CU (measured r01: a
@@ -564,7 +563,6 @@ Plan plan(const rdn_wgrad_desc* d) {
     for (int c : cands)
       if (d->ndim % c == 0 && c * bm <= maxacc) { p.ck = c; p.rows = 1; p.bm = bm; break; }
   }
-#endif
   p.chunks_rows = d->ndim / p.ck;   // the PReLU-gate fusion decision (rdn_wgrad_chunks) is made on these
   p.glds = 0;
   p.tiles_x = (d->w + TW - 1) / TW;

@@ -114,9 +114,9 @@ class GradSync:
         # `pending` for the caller's clip (take_pending) instead of scaling
         self.defer_average = False
         self.pending = None
-        # set to a list to time each finish(): (backward done on the compute stream,
-        # last bucket's all-reduce done on the comm stream) event pairs -- the
-        # all-reduce time the backward did not hide (bench.py exposed_allreduce_ms)
+        # set to a list to time each finish(): (backward done, last bucket's all-reduce
+        # done) event pairs on the compute stream -- the all-reduce time the backward did
+        # not hide (bench.py exposed_allreduce_ms)
         self.timing = None
 
     # --- engine hooks -------------------------------------------------
@@ -175,14 +175,18 @@ class GradSync:
             if not self._launched[b] and self.overlap:
                 self._srcs[b].append(torch.cuda.current_stream())
             self._launch(b)
-        if e0 is not None:
-            e1 = torch.cuda.Event(enable_timing=True)
-            e1.record(self.stream)                    # behind the last bucket's all-reduce
-            self.timing.append((e0, e1))
         for w in self._works:
             w.wait()
         if self.overlap:
             torch.cuda.current_stream().wait_stream(self.stream)
+        if e0 is not None:
+            # (ProcessGroupNCCL runs an async all-reduce on its own stream, which waits on
+            # self.stream -- not the other way round: an event on self.stream marks only
+            # the launch.  w.wait() made the current stream wait on the collectives, so an
+            # event recorded here completes when the last all-reduce has)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record(torch.cuda.current_stream())
+            self.timing.append((e0, e1))
         self._works = []
         if self.world > 1:
             if self.defer_average:
