@@ -10,7 +10,8 @@ Each step is checked against the CPU oracle's train step (oracle/rdunet_ref.py
 train_step, diffusion_RDUnet.py:76-115) at that step's shape, from the GPU's
 parameters just before it: fp32 loss <= 1e-6 relative, every clipped gradient tensor
 <= 1e-3 rel-L2 (the budget of test_gpu_fullsize.py: two fp32 rounding paths, each up
-to 6e-4 from fp64 per tensor), the flat gradient <= 3e-4 (at batch 2
+to 6e-4 from fp64 per tensor) -- or, on a step where a tensor exceeds
+that, every tensor <= 2e-3 against the fp64 oracle (below) --, the flat gradient <= 3e-4 (at batch 2
 the gradient averages 2 images, not 16: measured 1e-5..1e-4).  The
 AdamW update applied inside the replay is checked against torch.optim.AdamW's update
 of the same parameters with the same (GPU) gradient (<= 1e-5 relative on the deltas),
@@ -101,15 +102,19 @@ def test_mixed_128_256_stream_train_graphs_vs_oracle():
         assert lrel <= 1e-6
         assert flat <= 3e-4
         if worst[0] > 1e-3:
-            # a PReLU-slope gradient (sum of pre*dY over the negative pixels) can cancel
-            # to a small norm where fp32 summation order alone moves it by 1e-3 (SURVEY
-            # §7: the reference's own fp32 gradients reach 6e-4 against fp64): judge
-            # such a tensor against the fp64 oracle, beside the fp32 oracle's own error
+            # A PReLU-slope gradient (sum of pre*dY over the negative pixels) can cancel to
+            # a small norm where fp32 summation order alone moves it by ~1e-3: the
+            # reference's own fp32 gradients reach 6e-4 from fp64 on block_2_0.* (SURVEY.md
+            # section 7), and two independent fp32 paths (GPU, oracle) each that far from
+            # fp64 can sit 1.2e-3 apart -- what round 5 saw (1.73e-3 on
+            # block_2_0.actv_0.weight).  So such a step is judged against the fp64 oracle
+            # instead, per tensor at SURVEY section 7's bound: <= 2e-3 rel-L2 (a fixed cap,
+            # not a multiple of the fp32 oracle's own error)
             _, _, g64, _ = R.train_step({k: v.double() for k, v in before.items()}, clean.cpu().double(),
                                         noisy.cpu().double(), t, 20, clip_value=1.0)
             for k in ref_g:
-                e_gpu, e_ref = _rel(got_g[k], g64[k]), _rel(ref_g[k], g64[k])
-                assert e_gpu <= max(1e-3, 4 * e_ref), (k, e_gpu, e_ref)
+                e_gpu = _rel(got_g[k], g64[k])
+                assert e_gpu <= 2e-3, (k, e_gpu, _rel(ref_g[k], g64[k]))
         assert drel <= 1e-5
     assert shapes == [128, 256, 128, 256]
     assert graphs.captures == 2 and len(graphs.graphs) == 2
