@@ -25,7 +25,7 @@
  *   rdn_conv_wgrad /  aten convolution_backward grad_weight for the same convs.
  *   rdn_wgrad_reduce
  *   rdn_conv_dgrad_wgrad  both of the above for one gated level-0 conv in one pass.
- *   rdn_dense3_fwd    conv_0..conv_2 (+ PReLU, + torch.cat) of a level-0 DenoisingBlock
+ *   rdn_dense3_fwd    conv_0..conv_2 (+ PReLU, + torch.cat) of a level-0 / level-1 DenoisingBlock
  *                     in one pass, Unet_model.py:81-87.
  *   rdn_prelu_bwd     aten _prelu_kernel_backward (dx, dalpha) + conv grad_bias.
  *   rdn_interp        x = a*noisy + (1-a)*clean, diffusion_RDUnet.py:90-100, :33-36.
@@ -216,13 +216,19 @@ int rdn_conv_dgrad_wgrad_kernel_name(const rdn_conv_desc* dgrad, const rdn_wgrad
    channels 16-31 x_pl elements further; channel-blocked, 16-channel planes);
    out[k]: the plane receiving conv_k's output (pixel stride 16); pre[k]: its PReLU
    input, plain [pixels][16]; wp[k]: packed forward weights (rdn_pack_weights with
-   ck = cin, kp[k] columns).  H % 8 == 0, W % 16 == 0. */
+   ck = cin, kp[k] columns).  H % 8 == 0, W % 16 == 0.
+   x_c = 64 (round 6): the level-1 block (x 64 channels, growth 32, 32-channel planes:
+   x channels 32-63 x_pl elements after 0-31, out[k] pixel stride 32, pre[k] plain
+   [pixels][32], wp[k] packed by rdn_pack_weights CONV_FWD with the rdn_conv3_chunk
+   K order of cin = 64 / 96 / 128: kp >= 576 / 896 / 1152); H % 16 == 0, W % 16 == 0.
+   x_c = 0 or 32: the level-0 form above. */
 typedef struct rdn_dense3_desc {
   int32_t n, h, w;
   const void* x; int64_t x_pl;
   void* out[3]; void* pre[3];
   const void* wp[3]; int32_t kp[3];
   const float* bias[3]; const float* alpha[3];
+  int32_t x_c;
 } rdn_dense3_desc;
 int rdn_dense3_fwd(const rdn_dense3_desc* d, void* stream);
 /* name of the instantiation (tile geometry: 8x16, 16x16 or 8x32 output pixels, env

@@ -45,6 +45,32 @@ def test_struct_layout_matches_header():
     body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
     names = re.findall(r"\**\s*([a-z_0-9]+)\s*[,;]", body)
     assert names == [f for f, _ in H.WgradDesc._fields_]
+    body = re.search(r"typedef struct rdn_dense3_desc \{(.*?)\} rdn_dense3_desc;", src, re.S).group(1)
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    names = re.findall(r"\**\s*([a-z_0-9]+)\s*(?:\[\d+\])?\s*[,;]", body)
+    assert names == [f for f, _ in H.Dense3Desc._fields_]
+
+
+def test_dense3_level_validation_on_host():
+    """rdn_dense3_fwd rejects an unknown x_c and a level-1 descriptor with short packed
+    K before anything is launched (no GPU needed)."""
+    import ctypes
+    from vub_image_denoising_amd import _hip as H
+    lib = H.load_library()
+    d = H.Dense3Desc()
+    d.n, d.h, d.w = 1, 32, 32
+    d.x, d.x_pl = 4096, 32 * 32 * 32
+    for k in range(3):
+        d.out[k] = d.pre[k] = d.wp[k] = 4096 * (k + 2)
+        d.bias[k] = d.alpha[k] = 4096
+    d.kp[0], d.kp[1], d.kp[2] = 576, 896, 1152
+    d.x_c = 48
+    assert lib.rdn_dense3_fwd(ctypes.byref(d), None) == -1 and b"x_c" in lib.rdn_last_error()
+    d.x_c = 64
+    d.kp[1] = 864   # conv_1 needs the packed K of 96 channels rounded to 64: 896
+    assert lib.rdn_dense3_fwd(ctypes.byref(d), None) < 0 and b"packed K" in lib.rdn_last_error()
+    d.kp[1], d.h = 896, 24   # level-1 grid must be a multiple of 16
+    assert lib.rdn_dense3_fwd(ctypes.byref(d), None) < 0 and b"H % 16" in lib.rdn_last_error()
 
 
 def test_state_dict_keys_and_shapes_match_oracle_spec():

@@ -29,9 +29,11 @@ def _run(fuse, B, Hh, Ww, seed=0):
         y = m(x, t)
         (y * w).mean().backward()
         grads = {n: p.grad.detach().clone() for n, p in m.named_parameters()}
-        fused = sum("dense3" in L.extra for pool in m._rdn_engines.values() for eng in pool for L in eng.layers)
+        # (level 0 only: the level-1 blocks' fused launch, round 6, is tests/test_gpu_dense1.py's)
+        fused = sum("dense3" in L.extra and L.level == 0 for pool in m._rdn_engines.values() for eng in pool
+                    for L in eng.layers)
         keys = {L.extra["info"]["dense3"][2] for pool in m._rdn_engines.values() for eng in pool for L in eng.layers
-                if L.extra.get("info", {}).get("dense3")}
+                if L.level == 0 and L.extra.get("info", {}).get("dense3")}
         with torch.no_grad():   # inference engine (no PReLU inputs kept)
             y_inf = m(x, t)
         return y.detach().clone(), y_inf, grads, fused, keys

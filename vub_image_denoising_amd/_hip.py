@@ -62,6 +62,7 @@ class Dense3Desc(C.Structure):
         ("out", _vp * 3), ("pre", _vp * 3),
         ("wp", _vp * 3), ("kp", _i32 * 3),
         ("bias", _vp * 3), ("alpha", _vp * 3),
+        ("x_c", _i32),
     ]
 
 

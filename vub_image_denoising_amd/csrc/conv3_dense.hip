@@ -342,6 +342,11 @@ extern "C" int rdn_dense3_fwd(const rdn_dense3_desc* d, void* stream) {
       rdn_set_error("rdn_dense3_fwd: conv %d: null or unaligned operand", k);
       return RDN_E_ARG;
     }
+  if (d->x_c == 64) return rdn_dense3_l1_launch(d, (hipStream_t)stream);   // level 1 (conv3_dense1.hip)
+  if (d->x_c != 0 && d->x_c != 32) {
+    rdn_set_error("rdn_dense3_fwd: x_c %d (32: level 0, 64: level 1)", d->x_c);
+    return RDN_E_ARG;
+  }
   if (d->kp[0] < W0::KC || d->kp[1] < W1::KC || d->kp[2] < W2::KC) {
     rdn_set_error("rdn_dense3_fwd: packed K too small (pack with ck = cin)");
     return RDN_E_SHAPE;

@@ -154,6 +154,7 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
 int rdn_conv3_launch(const rdn_conv_desc* d, hipStream_t st);
 int rdn_conv3_chunk_impl(int cin, int dtype);
 int rdn_conv3_chunk_pow2(int cin, int cap);
+int rdn_dense3_l1_launch(const rdn_dense3_desc* d, hipStream_t st);
 int rdn_conv3_ws_launch(const rdn_conv_desc* d, int ck, hipStream_t st);
 int rdn_conv3_wsd_launch(const rdn_conv_desc* d, int ck, hipStream_t st);
 int rdn_conv3_big_launch(const rdn_conv_desc* d, int ck, hipStream_t st);

@@ -239,6 +239,9 @@ REDUCE_BATCH = os.environ.get("RDN_REDUCE_BATCH", "1") != "0"
 # conv_0..conv_2 of every level-0 DenoisingBlock (base_filters 32, bf16) as ONE
 # launch that reads x once and keeps out_0 / out_1 on chip (rdn_dense3_fwd)
 FUSE_DENSE = os.environ.get("RDN_DENSE", "1") != "0"
+# round 6: the level-1 blocks' conv_0..2 as one launch too (conv3_dense1.hip); RDN_DENSE1=0
+# keeps them on the three rdn_conv_fwd launches (A/B)
+FUSE_DENSE1 = os.environ.get("RDN_DENSE1", "1") != "0"
 
 
 def find_flat(params):
@@ -723,36 +726,45 @@ class UNetEngine:
             L.fwd_desc = d
 
     def _plan_dense3(self):
-        """Level-0 dense blocks whose conv_0..conv_2 forward runs as one
-        rdn_dense3_fwd launch (Unet_model.py:81-87 with x = 32 channels, growth 16):
-        the three layers read the block buffer's channel prefix (channel-blocked,
-        16-channel planes) and write its next planes; the launch goes at conv_0, the
-        other two are skipped."""
-        if not FUSE_DENSE or self.code != H.RDN_BF16 or self.H % 8 or self.W % 16:
+        """Dense blocks whose conv_0..conv_2 forward runs as one rdn_dense3_fwd launch
+        (Unet_model.py:81-87): level 0 (x = 32 channels, growth 16, 16-channel planes)
+        and, round 6, level 1 (x = 64 channels, growth 32, 32-channel planes; the
+        level-1 grid a multiple of 16).  The three layers read the block buffer's
+        channel prefix and write its next planes; the launch goes at conv_0, the other
+        two are skipped."""
+        if not FUSE_DENSE or self.code != H.RDN_BF16:
             return
         by_name = {L.name: L for L in self.layers}
         for L0 in self.layers:
-            if not L0.name.endswith(".conv_0") or L0.kind != "c3" or L0.level != 0:
+            if not L0.name.endswith(".conv_0") or L0.kind != "c3" or L0.level not in (0, 1):
                 continue
+            lvl = L0.level
+            if lvl == 1 and not FUSE_DENSE1:
+                continue
+            n, h, w = self.grid[lvl]
+            if (lvl == 0 and (h % 8 or w % 16)) or (lvl == 1 and (h % 16 or w % 16)):
+                continue
+            g, x_c = (16, 32) if lvl == 0 else (32, 64)
             blk = L0.name[:-len(".conv_0")]
             Ls = [by_name.get(f"{blk}.conv_{k}") for k in range(3)]
-            if any(L is None or L.kind != "c3" or L.level != 0 for L in Ls):
+            if any(L is None or L.kind != "c3" or L.level != lvl for L in Ls):
                 continue
             buf = L0.src.buf
             ps, pl = self.geo[buf]
-            if (ps != 16 or not pl or any(L.src.buf != buf or L.src.c0 != 0 or L.dst is None or L.dst.buf != buf
-                                            or L.cout != 16 or L.cout_pad != 16 or L.resid is not None for L in Ls)
-                    or [L.cin for L in Ls] != [32, 48, 64] or [L.dst.c0 for L in Ls] != [32, 48, 64]):
+            if (ps != g or not pl or any(L.src.buf != buf or L.src.c0 != 0 or L.dst is None or L.dst.buf != buf
+                                           or L.cout != g or L.cout_pad != g or L.resid is not None for L in Ls)
+                    or [L.cin for L in Ls] != [x_c, x_c + g, x_c + 2 * g]
+                    or [L.dst.c0 for L in Ls] != [x_c, x_c + g, x_c + 2 * g]):
                 continue
             d = H.Dense3Desc()
-            n, h, w = self.grid[0]
             d.n, d.h, d.w = n, h, w
+            d.x_c = x_c
             d.x, d.x_pl = self.bufs[buf].data_ptr(), pl
             for k, L in enumerate(Ls):
                 ptr, _, c0, _ = self._slice(L.dst)
                 d.out[k] = ptr + 2 * (c0 // ps) * pl
                 pre = self.bufs.get(L.pre)
-                d.pre[k] = pre.data_ptr() if pre is not None else self._dense_scratch(L.pre)
+                d.pre[k] = pre.data_ptr() if pre is not None else self._dense_scratch(L.pre, lvl, g)
                 packed = L.pack_fwd[8]
                 d.wp[k], d.kp[k] = packed.data_ptr(), packed.shape[1]
                 d.bias[k] = self.named[L.name + ".bias"].data_ptr()
@@ -761,12 +773,14 @@ class UNetEngine:
             for L in Ls[1:]:
                 L.extra["dense3_skip"] = True
 
-    def _dense_scratch(self, name):
+    def _dense_scratch(self, name, lvl=0, g=16):
         """PReLU-input target of a fused launch in an inference engine (no PRE_
-        buffers kept): one shared scratch plane, written and never read."""
+        buffers kept): one shared scratch plane per level, written and never read."""
         if not hasattr(self, "_pre_scratch"):
-            self._pre_scratch = torch.empty(self.P[0] * 16, dtype=self.dtype, device=self.device)
-        return self._pre_scratch.data_ptr()
+            self._pre_scratch = {}
+        if lvl not in self._pre_scratch:
+            self._pre_scratch[lvl] = torch.empty(self.P[lvl] * g, dtype=self.dtype, device=self.device)
+        return self._pre_scratch[lvl].data_ptr()
 
     def _build_bwd(self):
         lib = H.lib()
@@ -1080,7 +1094,7 @@ class UNetEngine:
                 # 6th entry: the fused launch's own minimal bytes (x read once, each
                 # conv's output and PReLU input written once: 32 + 3 x 32 channels)
                 Ls = [by_name[f"{blk}.conv_{k}"] for k in range(3)]
-                fused_min = es * self.P[0] * (Ls[0].cin + sum(2 * x.cout for x in Ls))
+                fused_min = es * self.P[L.level] * (Ls[0].cin + sum(2 * x.cout for x in Ls))
                 L.extra["info"]["dense3"] = ("fwd", f"{blk}.conv_0-2", self._dense3_key(L.extra["dense3"]),
                                              sum(p[3] for p in parts), sum(p[4] for p in parts), fused_min)
 
