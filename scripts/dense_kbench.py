@@ -2,7 +2,9 @@
 level-0 DenoisingBlock descriptors, timed for several builds of the library in one
 process (e.g. its -DDN_DIAG_* diagnostic builds, which remove one part of the work).
 
-    python scripts/dense_kbench.py build/variants/lib_a.so ... [B]
+    python scripts/dense_kbench.py build/variants/lib_a.so ... [B] [l1]
+
+(l1: the level-1 launch, conv3_dense1.hip, and its -DDN1_DIAG_* builds)
 """
 import ctypes as C
 import json
@@ -36,7 +38,8 @@ def main():
     train_step_device(m, x, x + 0.1, opt, "uniform", 1.0)
     torch.cuda.synchronize()
     eng = m.unet._rdn_engines[(batch, 256, 256, torch.bfloat16, True)][0]
-    desc = next((L.extra["dense3"] for L in eng.layers if "dense3" in L.extra), None)
+    lvl = 1 if "l1" in sys.argv[1:] else 0
+    desc = next((L.extra["dense3"] for L in eng.layers if "dense3" in L.extra and L.level == lvl), None)
     if desc is None:
         raise SystemExit("no dense3 descriptor on the engine")
     st = H.stream_ptr()
@@ -53,7 +56,7 @@ def main():
             torch.cuda.synchronize()
             us = 1e3 * s.elapsed_time(e) / 20
             res[name] = min(res.get(name, 1e9), round(us, 2))
-    print(json.dumps({"batch": batch, **res}))
+    print(json.dumps({"batch": batch, "level": lvl, **res}))
 
 
 if __name__ == "__main__":

@@ -112,6 +112,12 @@ __device__ __forceinline__ int opq(int v) {
   asm volatile("" : "+v"(v));
   return v;
 }
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+// two floats -> one bf16 pair by a single v_cvt_pk_bf16_f32 (RNE, as the scalar casts)
+__device__ __forceinline__ unsigned cvt_pk_bf16(f32x2 v) {
+  return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2));
+}
 __device__ __forceinline__ unsigned lds_addr(const unsigned char* p) {
   return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) unsigned char*)p;
 }
@@ -178,21 +184,29 @@ __global__ __launch_bounds__(NT, 1) void conv3_dense1_kernel(rdn_dense3_desc d, 
     return q;
   };
 
-  // ---- x region DMA: piece pc (1 KB) of tile tt; slot S = 64 pc + lane -> row S / XROW,
-  // pixel (S % XROW) / 9, unit (S % XROW) % 9 (unit 8 and the row pad: zero line)
-  auto issue_x = [&](int tt, int pc) {
-    const Tile q = tile_of(tt);
-    const void* src = (const void*)g_dn1_zero;
-    unsigned dst = lds_addr(lds + OFF_DUMP);
-    if (pc < X_PIECES) {
-      dst = lds_addr(lds + OFF_X) + pc * 1024;
-      const int S = opq(pc * 64 + lane);
-      const int ry = S / XROW, rem = S - ry * XROW, rx = rem / 9, u = rem - rx * 9;
-      const int gy = q.y0 - 3 + ry, gx = q.x0 - 3 + rx;
-      if (ry < XR && rx < XC && u < 8 && (unsigned)gy < (unsigned)H && (unsigned)gx < (unsigned)W)
-        src = X + (u >> 2) * d.x_pl + (((int64_t)q.n * H + gy) * W + gx) * 32 + (u & 3) * 8;
-    }
-    glds16(src, dst);
+  // ---- x region DMA: piece pc = wave + 8 i (1 KB) of a tile; slot S = 64 pc + lane -> row
+  // S / XROW, pixel (S % XROW) / 9, unit (S % XROW) % 9 (unit 8 and the row pad: zero
+  // line).  The per-lane geometry is tile-invariant and computed once (the per-piece
+  // divisions and 64-bit address arithmetic were ~50 VALU per piece and tile): the source
+  // offset from the region origin (-1: a pad slot) and the region pixel ry << 8 | rx.
+  int xrel[XPW], xyx[XPW];
+#pragma unroll
+  for (int i = 0; i < XPW; ++i) {
+    const int pc = wave + NW * i, S = pc * 64 + lane;
+    const int ry = S / XROW, rem = S - ry * XROW, rx = rem / 9, u = rem - rx * 9;
+    const bool ok = pc < X_PIECES && ry < XR && rx < XC && u < 8;
+    xrel[i] = ok ? (u >> 2) * (int)d.x_pl + (ry * W + rx) * 32 + (u & 3) * 8 : -1;
+    xyx[i] = ry << 8 | rx;
+  }
+  auto issue_x = [&](const Tile& q, int i) {
+    const int pc = wave + NW * i;   // wave-uniform
+    const unsigned dst = pc < X_PIECES ? lds_addr(lds + OFF_X) + pc * 1024 : lds_addr(lds + OFF_DUMP);
+    const bf16* const base = X + (((int64_t)q.n * H + q.y0 - 3) * W + q.x0 - 3) * 32;
+    const bool interior = q.y0 >= 3 && q.y0 + TH + 3 <= H && q.x0 >= 3 && q.x0 + TW + 3 <= W;
+    bool ok = xrel[i] >= 0;
+    if (!interior)
+      ok = ok && (unsigned)(q.y0 - 3 + (xyx[i] >> 8)) < (unsigned)H && (unsigned)(q.x0 - 3 + (xyx[i] & 255)) < (unsigned)W;
+    glds16(ok ? (const void*)(base + xrel[i]) : (const void*)g_dn1_zero, dst);
   };
   // ---- weight chunk c (0..20) into ring slot c % 3: this wave's piece = rows 4w..4w+3
   const int wrow = 4 * wave + (lane >> 4);
@@ -213,7 +227,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dense1_kernel(rdn_dense3_desc d, 
 
   // ---- prologue: tile t's x, chunks 0 and 1
 #pragma unroll
-  for (int i = 0; i < XPW; ++i) issue_x(t, wave + NW * i);
+  for (int i = 0; i < XPW; ++i) issue_x(tile_of(t), i);
   issue_w(std::integral_constant<int, 0>{});
   issue_w(std::integral_constant<int, 1>{});
   wait_vm<0>();
@@ -233,7 +247,6 @@ __global__ __launch_bounds__(NT, 1) void conv3_dense1_kernel(rdn_dense3_desc d, 
       const int m = K == 2 ? wave + 4 * sl : wave + 8 * sl;
       int y, x;
       mt_pixel<K>(m < NMT[K] ? m : 0, opq(j32), y, x);
-      // x coords of output pixel (y, x), tap (0, 0): (y + SH, x + SH); OUT coords = x coords - 1
       bx[sl] = ((y + SH[K]) * XROW + (x + SH[K]) * 9 + h) * 16;
       bo[sl] = ((y + SH[K] - 1) * OROW + (x + SH[K] - 1) * 9 + h) * 16;
       acc[sl] = (f32x16)(0.f);
@@ -250,36 +263,80 @@ __global__ __launch_bounds__(NT, 1) void conv3_dense1_kernel(rdn_dense3_desc d, 
     return from_out ? (dy * OROW + dx * 9 + 2 * cg) * 16 : (dy * XROW + dx * 9 + 2 * cg) * 16;
   };
 
-  // MFMAs of chunk step C for NS slots
+  // MFMAs of chunk step C for NS slots.  (Every fragment of the step read into
+  // registers before its first MFMA, 232 VGPRs: 152 -> 162 us per launch at B32, not
+  // kept -- the LDS latency is not what bounds this kernel)
   auto compute = [&](auto CC, auto NSC) {
     constexpr int C = decltype(CC)::value, NS = decltype(NSC)::value;
     constexpr int K = conv_of(C), J = C - CH0[K];
+    constexpr int NK = NSTEP[K] - 8 * J < 8 ? NSTEP[K] - 8 * J : 8;
     const unsigned char* const ring = lds + OFF_RING + (C % 3) * CHUNK;
 #pragma unroll
-    for (int s8 = 0; s8 < 8; ++s8) {
+    for (int s8 = 0; s8 < NK; ++s8) {
       const int s = 8 * J + s8;
-      if (s >= NSTEP[K]) break;   // (compile time)
       bool fo = false;
       const int bofs = bsrc(K, s, fo);
+#ifdef DN1_DIAG_NO_LDSRD   // diagnostic build (scripts/dense_kbench.py l1): opaque operands
+      u32x4 a, b[2];
+      asm volatile("" : "=v"(a));
+#pragma unroll
+      for (int sl = 0; sl < NS; ++sl) asm volatile("" : "=v"(b[sl]));
+      (void)bofs;
+#else
       const u32x4 a = *(const u32x4*)(ring + aoff[s8]);
       u32x4 b[2];
 #pragma unroll
       for (int sl = 0; sl < NS; ++sl)
         b[sl] = *(const u32x4*)(lds + (fo ? OFF_OUT + bo[sl] : OFF_X + bx[sl]) + bofs);
+#endif
+#ifdef DN1_DIAG_NO_MFMA   // diagnostic build: operands consumed without MFMAs
+#pragma unroll
+      for (int sl = 0; sl < NS; ++sl) asm volatile("" ::"v"(a), "v"(b[sl]));
+#else
 #pragma unroll
       for (int sl = 0; sl < NS; ++sl)
         acc[sl] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b[sl]),
                                                           acc[sl], 0, 0, 0);
+#endif
     }
   };
 
+  // epilogue geometry of conv K's two slots (tile-invariant, computed once): the global
+  // byte offset of the lane's 16-B unit in the tile (RDN_OOB: halo pixel or no m-tile),
+  // the OUT-grid LDS byte offset of its unit for the next conv (conv_0 / conv_1; -1: no
+  // m-tile) and its tile pixel (ty + 8) << 8 | (tx + 8) for the in-image test of
+  // border tiles
+  int eo[3][2], el[2][2], eyx[3][2];
+  auto epi_geo = [&](auto KC) {
+    constexpr int K = decltype(KC)::value;
+#pragma unroll
+    for (int sl = 0; sl < 2; ++sl) {
+      const int m = K == 2 ? wave + 4 * sl : wave + 8 * sl;
+      const bool live = K == 2 ? (wave < 4) : (m < NMT[K]);
+      int y, x;
+      mt_pixel<K>(live ? m : 0, j32, y, x);
+      const int ty = y - (2 - SH[K]), tx = x - (2 - SH[K]);   // tile coordinates
+      const bool own = live && (unsigned)ty < (unsigned)TH && (unsigned)tx < (unsigned)TW;
+      eo[K][sl] = own ? ((ty * W + tx) * 32 + 8 * h) * 2 : RDN_OOB;
+      eyx[K][sl] = (ty + 8) << 8 | (tx + 8);
+      if constexpr (K < 2)   // OUT coords of conv K's output pixel: (y + SH, x + SH)
+        el[K][sl] = live ? ((y + SH[K]) * OROW + (x + SH[K]) * 9 + 4 * K + h) * 16 : -1;
+    }
+  };
+  epi_geo(std::integral_constant<int, 0>{});
+  epi_geo(std::integral_constant<int, 1>{});
+  epi_geo(std::integral_constant<int, 2>{});
+
   // epilogue of conv K for tile q: every lane issues 8 stores (2 slots x {pre, out} x 2
-  // units; slots without an m-tile and pixels outside the tile store at the OOB offset)
+  // units; slots without an m-tile and pixels outside the tile store at the OOB offset).
+  // Bias add and PReLU slope products as packed fp32 pairs, bf16 pairs by one
+  // v_cvt_pk_bf16_f32 each (the same rounding as the per-element casts)
   auto epilogue = [&](auto KC, const Tile& q) {
     constexpr int K = decltype(KC)::value;
     const int64_t pix0 = ((int64_t)q.n * H + q.y0) * W + q.x0;
     const __amdgpu_buffer_rsrc_t rp = rdn_rsrc((const bf16*)d.pre[K] + pix0 * 32);
     const __amdgpu_buffer_rsrc_t ro = rdn_rsrc((const bf16*)d.out[K] + pix0 * 32);
+    const bool border = q.y0 == 0 || q.x0 == 0 || q.y0 + TH >= H || q.x0 + TW >= W;
     const float* const bk = bal + K * 64;
     f32x4 bb[4], aa[4];
 #pragma unroll
@@ -289,25 +346,15 @@ __global__ __launch_bounds__(NT, 1) void conv3_dense1_kernel(rdn_dense3_desc d, 
     }
 #pragma unroll
     for (int sl = 0; sl < 2; ++sl) {
-      const int m = K == 2 ? wave + 4 * sl : wave + 8 * sl;
-      const bool live = K == 2 ? (wave < 4) : (m < NMT[K]);
-      int y, x;
-      mt_pixel<K>(live ? m : 0, opq(j32), y, x);
-      const int ty = y - (2 - SH[K]), tx = x - (2 - SH[K]);   // tile coordinates
-      const bool own = live && (unsigned)ty < (unsigned)TH && (unsigned)tx < (unsigned)TW;
-      const bool inimg = (unsigned)(q.y0 + ty) < (unsigned)H && (unsigned)(q.x0 + tx) < (unsigned)W;
       unsigned pk[8], ok[8];   // bf16 pairs: [2 i + e] = channels 8 i + 4 h + 2 e, + 1
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
-          float v0 = acc[sl][4 * i + 2 * e] + bb[i][2 * e], v1 = acc[sl][4 * i + 2 * e + 1] + bb[i][2 * e + 1];
-          pk[2 * i + e] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)v0) |
-                          ((unsigned)__builtin_bit_cast(unsigned short, (bf16)v1) << 16);
-          v0 = v0 > 0.f ? v0 : aa[i][2 * e] * v0;
-          v1 = v1 > 0.f ? v1 : aa[i][2 * e + 1] * v1;
-          ok[2 * i + e] = (unsigned)__builtin_bit_cast(unsigned short, (bf16)v0) |
-                          ((unsigned)__builtin_bit_cast(unsigned short, (bf16)v1) << 16);
+          const f32x2 v = f32x2{acc[sl][4 * i + 2 * e], acc[sl][4 * i + 2 * e + 1]} + f32x2{bb[i][2 * e], bb[i][2 * e + 1]};
+          const f32x2 av = v * f32x2{aa[i][2 * e], aa[i][2 * e + 1]};
+          pk[2 * i + e] = cvt_pk_bf16(v);
+          ok[2 * i + e] = cvt_pk_bf16(f32x2{v[0] > 0.f ? v[0] : av[0], v[1] > 0.f ? v[1] : av[1]});
         }
       // pairs of 4-channel groups (0, 1) and (2, 3) -> 16-B units: lanes < 32 hold channels
       // 16 P .. 16 P + 7, lanes >= 32 16 P + 8 .. + 15
@@ -322,36 +369,47 @@ __global__ __launch_bounds__(NT, 1) void conv3_dense1_kernel(rdn_dense3_desc d, 
           ok[4 * P + e] = so[0];
           ok[4 * P + 2 + e] = so[1];
         }
-      int off = own ? ((ty * W + tx) * 32 + 8 * h) * 2 : RDN_OOB;
-      asm volatile("" : "+v"(off));
+      bool inimg = true;
+      if (border)
+        inimg = (unsigned)(q.y0 + (eyx[K][sl] >> 8) - 8) < (unsigned)H && (unsigned)(q.x0 + (eyx[K][sl] & 255) - 8) < (unsigned)W;
+      const int off = eo[K][sl];
 #pragma unroll
       for (int P = 0; P < 2; ++P) {
         const u32x4 up = {pk[4 * P], pk[4 * P + 1], pk[4 * P + 2], pk[4 * P + 3]};
         const u32x4 uo = {ok[4 * P], ok[4 * P + 1], ok[4 * P + 2], ok[4 * P + 3]};
         const int o = off == RDN_OOB ? RDN_OOB : off + 32 * P;
+#ifndef DN1_DIAG_NO_STORE   // diagnostic build: no global stores
         __builtin_amdgcn_raw_buffer_store_b128(up, rp, o, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b128(uo, ro, o, 0, 0);
-        if constexpr (K < 2) {   // the next conv's operand: OUT grid (x coords - 1), units (out_K: 4 K) + 2 P + h
-          if (live) {
+#else
+        asm volatile("" ::"v"(up), "v"(uo), "v"(o));
+#endif
+        if constexpr (K < 2) {   // the next conv's operand: OUT grid, units (out_K: 4 K) + 2 P + h
+          if (el[K][sl] >= 0) {
             const u32x4 z = inimg ? uo : u32x4{0u, 0u, 0u, 0u};
-            const int oy = y + SH[K], ox = x + SH[K];   // OUT coords of conv K's output pixel
-            *(u32x4*)(lds + OFF_OUT + (oy * OROW + ox * 9 + 4 * K + 2 * P + h) * 16) = z;
+            *(u32x4*)(lds + OFF_OUT + el[K][sl] + 32 * P) = z;
           }
         }
       }
     }
   };
 
-  auto step = [&](auto CC, const Tile& q, int t_next) {
+  auto step = [&](auto CC, const Tile& q, const Tile& qn) {
     constexpr int C = decltype(CC)::value;
     constexpr int K = conv_of(C);
     wait_vm<vm_after(C)>();   // chunk C landed (this wave's piece)
+#ifndef DN1_DIAG_NO_BAR       // diagnostic build (with NO_WDMA / NO_XDMA): no barriers
     bar_lds();                // every wave's piece; every wave done with step C - 1 (ring slot (C + 2) % 3)
+#endif
+#ifndef DN1_DIAG_NO_XDMA   // diagnostic build: every tile multiplies the first tile's x
     if constexpr (xdma_n(C) > 0) {
 #pragma unroll
-      for (int i = 0; i < xdma_n(C); ++i) issue_x(t_next, wave + NW * (xdma_first(C) + i));
+      for (int i = 0; i < xdma_n(C); ++i) issue_x(qn, xdma_first(C) + i);
     }
+#endif
+#ifndef DN1_DIAG_NO_WDMA   // diagnostic build: the ring keeps the prologue's chunks
     issue_w(std::integral_constant<int, (C + 2) % NSTEPS>{});
+#endif
     if constexpr (C == CH0[K]) conv_begin(std::integral_constant<int, K>{});
     const int ns = K == 0 ? ns0 : K == 1 ? ns1 : ns2;
     if (ns == 2) compute(CC, std::integral_constant<int, 2>{});
@@ -361,8 +419,8 @@ __global__ __launch_bounds__(NT, 1) void conv3_dense1_kernel(rdn_dense3_desc d, 
 
   for (;;) {
     const Tile q = tile_of(t);
-    const int t_next = min(t + per, t_last);   // (past the range: a harmless re-load of this tile)
-    for_steps([&](auto CC) { step(CC, q, t_next); }, std::make_integer_sequence<int, NSTEPS>{});
+    const Tile qn = tile_of(min(t + per, t_last));   // (past the range: a harmless re-load of this tile)
+    for_steps([&](auto CC) { step(CC, q, qn); }, std::make_integer_sequence<int, NSTEPS>{});
     t += per;
     if (t >= t_hi) break;
   }
@@ -377,7 +435,7 @@ int rdn_dense3_l1_launch(const rdn_dense3_desc* d, hipStream_t st) {
     rdn_set_error("rdn_dense3_fwd(level 1): packed K too small (kp %d %d %d)", d->kp[0], d->kp[1], d->kp[2]);
     return RDN_E_SHAPE;
   }
-  if (d->n <= 0 || d->h % TH || d->w % TW || ((uintptr_t)d->x & 15) || d->x_pl % 8 ||
+  if (d->n <= 0 || d->h % TH || d->w % TW || ((uintptr_t)d->x & 15) || d->x_pl % 8 || d->x_pl >= (1ll << 30) ||
       d->x_pl < (int64_t)d->n * d->h * d->w * 32) {
     rdn_set_error("rdn_dense3_fwd(level 1): needs H %% 16 == 0, W %% 16 == 0 and a channel-blocked x (32-channel planes)");
     return RDN_E_SHAPE;
