@@ -467,6 +467,8 @@ class Trainer:
         self.opt = FusedAdamW(self.model.parameters(), lr=1e-4, weight_decay=1e-4)
         if world > 1:
             self.unet._rdn_flat.grad_sync = GradSync(self.unet._rdn_flat, bucket_mb=25.0)
+            if graph:   # device-clock stamps around the all-reduce tail, replayed with the graph
+                self.unet._rdn_flat.grad_sync.stamps = torch.zeros(3, dtype=torch.int64, device=dev)
         self.graph = None
         if graph:   # the whole step as one hipGraph replay (train_graph.TrainStepGraph)
             from vub_image_denoising_amd.train_graph import TrainStepGraph
@@ -828,19 +830,37 @@ def main():
             sync.timing = []
         el, loss = tr.timed(args.steps, world, live)
         el_eager = el
-    exposed = None
-    if sync is not None:
-        mine = sync.exposed_ms()
-        sync.timing = None
+    exposed = exposed_graph = None
+
+    def over_ranks(mine, note):
         ex = torch.zeros(world, dtype=torch.float64)
         ex[rank] = -1.0 if mine is None else mine
         dist.all_reduce(ex, group=cpu_group)   # (each rank fills its own slot)
         per = [None if v < 0 else round(v, 4) for v in ex.tolist()]
         vals = [v for v in per if v is not None]
-        exposed = {"per_rank": per, "max": max(vals) if vals else None,
-                   "mean": round(sum(vals) / len(vals), 4) if vals else None, "unit": "ms per step",
-                   "note": "eager pass of the timed steps: end of the last gradient bucket's all-reduce on the "
-                           "comm stream minus the end of the backward on the compute stream (0 when hidden)"}
+        return {"per_rank": per, "max": max(vals) if vals else None,
+                "mean": round(sum(vals) / len(vals), 4) if vals else None, "unit": "ms per step", "note": note}
+    if sync is not None:
+        mine = sync.exposed_ms()
+        sync.timing = None
+        exposed = over_ranks(mine, "eager pass of the timed steps: end of the last gradient bucket's all-reduce "
+                                   "on the comm stream minus the end of the backward on the compute stream "
+                                   "(0 when hidden)")
+        if graph and sync.stamps is not None:
+            # the replayed step itself: its GradSync stamp kernels, read after each of
+            # `steps` further (untimed) replays
+            from vub_image_denoising_amd import _hip as H
+            from vub_image_denoising_amd.ddp import exposure_from_stamps
+            samples = []
+            for i in range(args.steps):
+                tr.step(i)
+                torch.cuda.synchronize()
+                samples.append(sync.stamps.tolist())
+            st = exposure_from_stamps(samples, H.lib().rdn_wall_clock_khz())
+            exposed_graph = over_ranks(None if st is None else st["mean"],
+                                       "hipGraph replays of the timed step: device-clock stamps on the compute "
+                                       "stream before and after its wait on the last all-reduce, less the launch "
+                                       "gap of two back-to-back stamps (ddp.exposure_from_stamps)")
     if world > 1:
         tt = torch.tensor([el, el_eager], device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -939,6 +959,7 @@ def main():
             "extra_configs": extra,
             "roofline": roof,
             "exposed_allreduce_ms": exposed,
+            "exposed_allreduce_ms_graph": exposed_graph,
             "peak_hbm_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 2),
             "cpu_baseline": cpu,
             "inference": infer,

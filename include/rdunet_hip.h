@@ -321,6 +321,13 @@ int rdn_adam_step(float* p, const float* g, float* m, float* v, int64_t count,
                   int64_t step, const int64_t* step_dev, float grad_scale, void* stream);
 /* *counter += 1 on the device (one thread; stream-ordered) */
 int rdn_counter_inc(int64_t* counter, void* stream);
+/* buf[slot] = the device wall clock (constant rate, rdn_wall_clock_khz ticks per ms) when
+   this launch starts on `stream`: stream-ordered timestamps that survive hipGraph capture
+   (the exposed all-reduce time of the replayed data-parallel step; no reference
+   counterpart -- the reference has no data parallelism) */
+int rdn_stamp(uint64_t* buf, int32_t slot, void* stream);
+/* ticks per millisecond of rdn_stamp's clock (hipDeviceAttributeWallClockRate, kHz), < 0 on error */
+int64_t rdn_wall_clock_khz(void);
 
 /* improved_sampling update: x = x - (c1*f1 + a*y) + (c2*f2 + ap*y), with c1 = 1-a and
    c2 = 1-ap rounded on the host exactly as the reference's Python scalars are */

@@ -145,3 +145,18 @@ def test_capture_drain_refuses_unsafe_nccl_groups(monkeypatch):
     monkeypatch.setenv("TORCH_NCCL_CUDA_EVENT_CACHE", "1")
     with pytest.raises(TG.GraphCaptureUnsafe, match="TORCH_NCCL_CUDA_EVENT_CACHE"):
         TG._drain_collectives(None)
+
+
+def test_exposure_from_stamps():
+    """bench.py's graph-path exposed all-reduce time from GradSync's replayed stamp
+    triples: (comm end - backward end) less the back-to-back stamp gap, floored at 0."""
+    from vub_image_denoising_amd.ddp import exposure_from_stamps
+    khz = 100_000   # 100 MHz clock: 100 ticks per microsecond
+    hidden = (1_000_000, 1_000_300, 1_000_600)        # gap 3 us both ways: nothing exposed
+    exposed = (2_000_000, 2_050_300, 2_050_600)       # 503 us to the all-reduce end, 3 us gap
+    early = (3_000_000, 3_000_100, 3_000_500)         # a slow stamp launch: floored at 0
+    st = exposure_from_stamps([hidden, exposed, early], khz)
+    assert st["per_step"] == [0.0, 0.5, 0.0]
+    assert st["max"] == 0.5 and abs(st["mean"] - 0.5 / 3) < 1e-4
+    assert abs(st["raw_mean"] - (0.003 + 0.503 + 0.001) / 3) < 1e-4
+    assert exposure_from_stamps([], khz) is None and exposure_from_stamps([hidden], 0) is None

@@ -140,13 +140,19 @@ def _rccl_worker(init_file, q):
         mE, oE = make(True)     # eager, RCCL
         mG, oG = make(True)     # graph, RCCL inside the capture
         mN, oN = make(False)    # graph, no GradSync
+        # device-clock stamps around the all-reduce tail, captured with the step (bench.py
+        # exposed_allreduce_ms_graph): read after each replay
+        mG.unet._rdn_flat.grad_sync.stamps = torch.zeros(3, dtype=torch.int64, device=dev)
         gG = TrainStepGraph(mG, oG, shape, t_input=True)
         gN = TrainStepGraph(mN, oN, shape, t_input=True)
         nb = len(mG.unet._rdn_flat.grad_sync.buckets)
+        samples = []
         for c, n, t in data:
             le = train_step_device(mE, c, n, oE, 'uniform', 1.0, t=t)
             oE.step()
             lg = gG(c, n, t).clone()
+            torch.cuda.synchronize()
+            samples.append(mG.unet._rdn_flat.grad_sync.stamps.tolist())
             ln = gN(c, n, t).clone()
             if not (torch.equal(le, lg) and torch.equal(lg, ln)):
                 raise AssertionError(f"losses differ: eager {le.item()} graph {lg.item()} nosync {ln.item()}")
@@ -161,6 +167,12 @@ def _rccl_worker(init_file, q):
             gs.begin()
             gs.finish()
         exposed = gs.exposed_ms()
+        from vub_image_denoising_amd import _hip as H
+        from vub_image_denoising_amd.ddp import exposure_from_stamps
+        khz = H.lib().rdn_wall_clock_khz()
+        ordered = all(0 < a <= b <= cc for a, b, cc in samples) and len({tuple(x) for x in samples}) == len(samples)
+        st = exposure_from_stamps(samples, khz)
+        exposed = (exposed, khz, ordered, st)
         res = (bool(torch.equal(fE, fG)), bool(torch.equal(fG, fN)), nb, gG.graph_nodes, exposed)
         dist.destroy_process_group()
         q.put(res)
@@ -182,10 +194,14 @@ def test_rccl_world1_graph_captured_gradsync(tmp_path):
         if p.is_alive():
             p.kill()
     assert not isinstance(res, str), res
-    same_eager, same_nosync, nb, nodes, exposed = res
+    same_eager, same_nosync, nb, nodes, (exposed, khz, ordered, st) = res
     print(f"RCCL world 1: {nb} buckets, graph nodes {nodes}; replay == eager: {same_eager}, == no-sync: {same_nosync}; "
-          f"unhidden all-reduce {exposed} ms")
+          f"unhidden all-reduce {exposed} ms; replayed stamps ({khz} kHz clock): {st}")
     assert nb > 1
     assert exposed is not None and exposed > 0.0
+    # the replayed stamps: every replay rewrote them, in stream order, and the graph-path
+    # exposure is a finite non-negative figure (small here: world 1, tiny buckets)
+    assert khz > 0 and ordered
+    assert st is not None and 0.0 <= st["mean"] < 50.0
     assert same_eager and same_nosync
     assert p.exitcode == 0

@@ -126,6 +126,8 @@ SIGNATURES = {
     "rdn_adam_step": (_i32, [_vp, _vp, _vp, _vp, _i64, C.c_double, C.c_double, C.c_double, C.c_double, C.c_double,
                              _i32, _i64, _vp, _f32, _vp]),
     "rdn_counter_inc": (_i32, [_vp, _vp]),
+    "rdn_stamp": (_i32, [_vp, _i32, _vp]),
+    "rdn_wall_clock_khz": (_i64, []),
     "rdn_sampling_combine": (_i32, [_vp, _vp, _vp, _vp, _i64, _f32, _f32, _f32, _f32, _vp]),
     "rdn_nchw_to_nhwc": (_i32, [_i32, _vp, _i32, _i32, _i32, _i32, _vp, _i64, _i32, _i64, _i32, _vp]),
     "rdn_nhwc_to_nchw": (_i32, [_i32, _vp, _i64, _i32, _i64, _i32, _i32, _i32, _i32, _vp, _i32, _vp]),

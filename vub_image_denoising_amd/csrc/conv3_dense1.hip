@@ -112,12 +112,6 @@ __device__ __forceinline__ int opq(int v) {
   asm volatile("" : "+v"(v));
   return v;
 }
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-// two floats -> one bf16 pair by a single v_cvt_pk_bf16_f32 (RNE, as the scalar casts)
-__device__ __forceinline__ unsigned cvt_pk_bf16(f32x2 v) {
-  return __builtin_bit_cast(unsigned, __builtin_convertvector(v, bf16x2));
-}
 __device__ __forceinline__ unsigned lds_addr(const unsigned char* p) {
   return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) unsigned char*)p;
 }
@@ -353,8 +347,8 @@ __global__ __launch_bounds__(NT, 1) void conv3_dense1_kernel(rdn_dense3_desc d, 
         for (int e = 0; e < 2; ++e) {
           const f32x2 v = f32x2{acc[sl][4 * i + 2 * e], acc[sl][4 * i + 2 * e + 1]} + f32x2{bb[i][2 * e], bb[i][2 * e + 1]};
           const f32x2 av = v * f32x2{aa[i][2 * e], aa[i][2 * e + 1]};
-          pk[2 * i + e] = cvt_pk_bf16(v);
-          ok[2 * i + e] = cvt_pk_bf16(f32x2{v[0] > 0.f ? v[0] : av[0], v[1] > 0.f ? v[1] : av[1]});
+          pk[2 * i + e] = rdn_cvt2(v[0], v[1]);
+          ok[2 * i + e] = rdn_cvt2(v[0] > 0.f ? v[0] : av[0], v[1] > 0.f ? v[1] : av[1]);
         }
       // pairs of 4-channel groups (0, 1) and (2, 3) -> 16-B units: lanes < 32 hold channels
       // 16 P .. 16 P + 7, lanes >= 32 16 P + 8 .. + 15

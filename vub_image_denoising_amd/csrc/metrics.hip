@@ -47,16 +47,25 @@ ColTiles col_tiles(int w) {
 
 // Block = txo output columns x TY output rows of one (image, channel) plane; thread
 // t owns input column ox0 - 3 + t.  The block walks its TY + 6 input rows once: each
-// row goes to a double-buffered LDS row (one barrier per row), thread t < txo
-// forms the horizontal 7-sums of the five moments (u, v, u^2, v^2, uv) of output
+// row goes to a double-buffered LDS row of (gt, x) pairs (one barrier per row), thread
+// t < txo forms the horizontal 7-sums of the five moments (u, v, u^2, v^2, uv) of output
 // column ox0 + t, keeps the last 7 rows of them in registers and sums those
 // (no running-sum subtraction: each window mean is a fresh 49-term sum, as
 // exact as the oracle's); the next 7 rows' loads are in flight meanwhile.
-__global__ __launch_bounds__(NT_MAX) void image_metrics_kernel(const float* __restrict__ gt,
+// The kernel is VALU-issue bound, so the moments go as packed fp32
+// pairs -- (u, v) and (u^2, v^2) by one v_pk_add_f32 / v_pk_fma_f32 each, in the same
+// per-lane order and rounding as the scalar form -- the SSIM quotient takes one
+// reciprocal (1 ulp) instead of the IEEE division sequence, and a thread's squared
+// errors and SSIM terms (<= 64 rows) are summed in fp32 and widened to float64 once,
+// for the block's float64 reduction.  Held to 5 waves per SIMD (94 VGPRs; the
+// unconstrained build took 164 and ran 3 per SIMD, too few to keep the row loads in
+// flight).  64 x 3 x 256^2 block pairs: 79 -> 48.5 us, 0.16 -> 0.26 of HBM (r06,
+// PMC: VALU instructions -34 %, wave cycles -31 %).
+__global__ __launch_bounds__(NT_MAX, 5) void image_metrics_kernel(const float* __restrict__ gt,
                                                                const float* __restrict__ x, int C, int H, int W,
                                                                int tiles_x, int TXO, int TY, float c1, float c2,
                                                                float cov_norm, double* __restrict__ part) {
-  __shared__ float rowbuf[2][2][NT_MAX];
+  __shared__ f32x2 rowbuf[2][NT_MAX];
   __shared__ double red[2][NT_MAX / 64];
   const int t = threadIdx.x;
   const int tile = blockIdx.x, c = blockIdx.y, n = blockIdx.z;
@@ -72,28 +81,33 @@ __global__ __launch_bounds__(NT_MAX) void image_metrics_kernel(const float* __re
   const int rows = TY + 2 * R;
   const int y_lo = oy0 > R ? oy0 : R, y_hi = (oy0 + TY < H - R) ? oy0 + TY : H - R;   // SSIM rows
 
-  // unconditional loads from a clamped (always valid) address, zeroed after:
-  // a load under a branch makes hipcc wait vmcnt(0) for it, which would drain
-  // the 7-row prefetch every row
-  const int xc = xi < 0 ? 0 : (xi >= W ? W - 1 : xi);
+  // buffer loads: a pixel outside the image (or past the last row) reads at an offset
+  // past the descriptor's range, which returns 0 -- no select after the load, so each
+  // row's value is waited for only where it is consumed and the 7-row prefetch stays
+  // in flight (a clamped load + select made hipcc wait for all seven at once)
+  const __amdgpu_buffer_rsrc_t rsa = rdn_rsrc(ga), rsb = rdn_rsrc(gb);
   auto load = [&](int r, float& a, float& b) {
     const int y = oy0 - R + r;
     const bool in = xin && (unsigned)y < (unsigned)H && r < rows;
-    const int yc = y < 0 ? 0 : (y >= H ? H - 1 : y);
-    const float va = ga[(int64_t)yc * W + xc], vb = gb[(int64_t)yc * W + xc];
-    a = in ? va : 0.f;
-    b = in ? vb : 0.f;
+    int o = in ? (y * W + xi) * 4 : RDN_OOB;
+    asm volatile("" : "+v"(o));
+    a = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsa, o, 0, 0));
+    b = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsb, o, 0, 0));
   };
   // rows r .. r+6 in flight: slot k of the register ring holds row r0 + k
-  float h[WIN][5];
+  f32x2 h01[WIN], h23[WIN];
+  float h4[WIN];
 #pragma unroll
-  for (int k = 0; k < WIN; ++k)
-#pragma unroll
-    for (int j = 0; j < 5; ++j) h[k][j] = 0.f;
-  double se = 0.0, ss = 0.0;
+  for (int k = 0; k < WIN; ++k) {
+    h01[k] = f32x2{0.f, 0.f};
+    h23[k] = f32x2{0.f, 0.f};
+    h4[k] = 0.f;
+  }
+  float se = 0.f, ss = 0.f;
   float pa[WIN], pb[WIN];
 #pragma unroll
   for (int k = 0; k < WIN; ++k) load(k, pa[k], pb[k]);
+  const f32x2 inv2 = {1.f / (WIN * WIN), 1.f / (WIN * WIN)};
   for (int r0 = 0; r0 < rows; r0 += WIN) {
 #pragma unroll
     for (int k = 0; k < WIN; ++k) {
@@ -104,50 +118,50 @@ __global__ __launch_bounds__(NT_MAX) void image_metrics_kernel(const float* __re
         const int y = oy0 - R + r;
         if (own_x && y >= oy0 && y < oy0 + TY && y < H) {
           const float d = a - b;
-          se += (double)(d * d);
+          se += d * d;
         }
-        float* const ra = rowbuf[r & 1][0];
-        float* const rb = rowbuf[r & 1][1];
-        ra[t] = a;
-        rb[t] = b;
+        f32x2* const rb = rowbuf[r & 1];
+        rb[t] = f32x2{a, b};
         __syncthreads();
         if (t < TXO) {
-          float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f, s4 = 0.f;
+          f32x2 s01 = {0.f, 0.f}, s23 = {0.f, 0.f};
+          float s4 = 0.f;
 #pragma unroll
           for (int q = 0; q < WIN; ++q) {
-            const float u = ra[t + q], v = rb[t + q];
-            s0 += u; s1 += v; s2 += u * u; s3 += v * v; s4 += u * v;
+            const f32x2 uv = rb[t + q];
+            s01 += uv;
+            s23 += uv * uv;
+            s4 = __builtin_fmaf(uv[0], uv[1], s4);
           }
-          h[k][0] = s0; h[k][1] = s1; h[k][2] = s2; h[k][3] = s3; h[k][4] = s4;
+          h01[k] = s01; h23[k] = s23; h4[k] = s4;
           const int yo = y - R;                 // output row whose window just completed
           if (r >= 2 * R && ssim_x && yo >= y_lo && yo < y_hi) {
-            float m[5];
+            f32x2 m01 = {0.f, 0.f}, m23 = {0.f, 0.f};
+            float m4 = 0.f;
 #pragma unroll
-            for (int j = 0; j < 5; ++j) {
-              float acc = 0.f;
-#pragma unroll
-              for (int q = 0; q < WIN; ++q) acc += h[(k + 1 + q) % WIN][j];   // rows yo-3 .. yo+3 in order
-              m[j] = acc;
+            for (int q = 0; q < WIN; ++q) {     // rows yo-3 .. yo+3 in order
+              m01 += h01[(k + 1 + q) % WIN];
+              m23 += h23[(k + 1 + q) % WIN];
+              m4 += h4[(k + 1 + q) % WIN];
             }
-            constexpr float inv = 1.f / (WIN * WIN);
-            const float ux = m[0] * inv, uy = m[1] * inv;
-            const float vx = cov_norm * (m[2] * inv - ux * ux);
-            const float vy = cov_norm * (m[3] * inv - uy * uy);
-            const float vxy = cov_norm * (m[4] * inv - ux * uy);
-            const float a1 = 2.f * ux * uy + c1, a2 = 2.f * vxy + c2;
-            const float b1 = ux * ux + uy * uy + c1, b2 = vx + vy + c2;
-            ss += (double)((a1 * a2) / (b1 * b2));
+            const f32x2 u = m01 * inv2;                       // (ux, uy)
+            const f32x2 v = cov_norm * (m23 * inv2 - u * u);  // (vx, vy)
+            const float vxy = cov_norm * (m4 * inv2[0] - u[0] * u[1]);
+            const float a1 = 2.f * u[0] * u[1] + c1, a2 = 2.f * vxy + c2;
+            const float b1 = u[0] * u[0] + u[1] * u[1] + c1, b2 = v[0] + v[1] + c2;
+            ss += (a1 * a2) * __builtin_amdgcn_rcpf(b1 * b2);
           }
         }
       }
     }
   }
-  // block reduction (wave shuffles, then the 4 wave sums in a fixed order)
+  // block reduction in float64 (wave shuffles, then the wave sums in a fixed order)
+  double sed = (double)se, ssd = (double)ss;
   for (int o = 32; o > 0; o >>= 1) {
-    se += __shfl_down(se, o, 64);
-    ss += __shfl_down(ss, o, 64);
+    sed += __shfl_down(sed, o, 64);
+    ssd += __shfl_down(ssd, o, 64);
   }
-  if ((t & 63) == 0) { red[0][t >> 6] = se; red[1][t >> 6] = ss; }
+  if ((t & 63) == 0) { red[0][t >> 6] = sed; red[1][t >> 6] = ssd; }
   __syncthreads();
   if (t == 0) {
     double a = 0.0, b = 0.0;
@@ -217,6 +231,7 @@ extern "C" int rdn_image_metrics(const float* gt, const float* x, int32_t n, int
     return RDN_E_SHAPE;
   }
   if (!(data_range > 0.f)) { rdn_set_error("rdn_image_metrics: data_range must be > 0"); return RDN_E_ARG; }
+  if ((int64_t)h * w >= (1ll << 29)) { rdn_set_error("rdn_image_metrics: planes of 2^29 pixels or more"); return RDN_E_SHAPE; }
   const ColTiles ct = col_tiles(w);
   const int tiles = tiles_of(n, c, h, w), ty = row_tile(n, c, h, w);
   const double rr = data_range;

@@ -452,6 +452,13 @@ __global__ void adam_kernel(float* __restrict__ p, const float* __restrict__ g, 
 
 __global__ void counter_inc_kernel(int64_t* c) { *c += 1; }
 
+// the device's constant-rate wall clock when this kernel starts, by one lane (vector
+// store): stream-ordered timestamps that a captured hipGraph replays (bench.py's
+// exposed all-reduce time of the replayed data-parallel step)
+__global__ void stamp_kernel(uint64_t* buf, int slot) {
+  if (threadIdx.x == 0) buf[slot] = wall_clock64();
+}
+
 // x_tilde = (1-a)*f1 + a*y; x_tilde_prev = (1-ap)*f2 + ap*y; x = x - x_tilde + x_tilde_prev
 // (diffusion_RDUnet.py:45-49), each product rounded separately as torch does.
 __global__ void sampling_combine_kernel(float* __restrict__ x, const float* __restrict__ f1, const float* __restrict__ f2,
@@ -656,6 +663,22 @@ extern "C" int rdn_counter_inc(int64_t* counter, void* stream) {
   if (!counter) { rdn_set_error("rdn_counter_inc: null"); return RDN_E_ARG; }
   counter_inc_kernel<<<1, 1, 0, RDN_STREAM>>>(counter);
   return rdn_check_launch("rdn_counter_inc");
+}
+
+extern "C" int rdn_stamp(uint64_t* buf, int32_t slot, void* stream) {
+  if (!buf || slot < 0) { rdn_set_error("rdn_stamp: bad arguments"); return RDN_E_ARG; }
+  stamp_kernel<<<1, 64, 0, RDN_STREAM>>>(buf, slot);
+  return rdn_check_launch("rdn_stamp");
+}
+
+extern "C" int64_t rdn_wall_clock_khz(void) {
+  int dev = 0, khz = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess ||
+      khz <= 0) {
+    rdn_set_error("rdn_wall_clock_khz: no device clock rate");
+    return RDN_E_LAUNCH;
+  }
+  return khz;
 }
 
 extern "C" int rdn_sampling_combine(float* x, const float* f1, const float* f2, const float* y, int64_t count, float c1,

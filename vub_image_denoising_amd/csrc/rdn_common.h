@@ -11,6 +11,15 @@ typedef __attribute__((ext_vector_type(4))) short i16x4;
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
 typedef __bf16 bf16;
+typedef __attribute__((ext_vector_type(2))) float f32x2;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+
+// two floats -> one dword of two bf16 (low, high) by ONE v_cvt_pk_bf16_f32 (RNE).  The
+// per-element form (two scalar casts, shift, or) compiles to two cvts with a zero second
+// operand plus the merge: 4 VALU per pair instead of 1, same bits
+__device__ __forceinline__ unsigned rdn_cvt2(float lo, float hi) {
+  return __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){lo, hi}, bf16x2));
+}
 
 #define RDN_LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
 
@@ -53,11 +62,7 @@ template <> struct Unit16<bf16> {
   __device__ static u32x4 pack(const float* f) {
     u32x4 u;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      unsigned short lo = __builtin_bit_cast(unsigned short, (bf16)f[2 * i]);
-      unsigned short hi = __builtin_bit_cast(unsigned short, (bf16)f[2 * i + 1]);
-      u[i] = (unsigned int)lo | ((unsigned int)hi << 16);
-    }
+    for (int i = 0; i < 4; ++i) u[i] = rdn_cvt2(f[2 * i], f[2 * i + 1]);
     return u;
   }
 };
@@ -107,11 +112,7 @@ __device__ __forceinline__ u32x2 rdn_ld8(__amdgpu_buffer_rsrc_t rs, bool ok, int
 __device__ __forceinline__ u32x2 rdn_pack4(const float* f) {
   u32x2 u;
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const unsigned short lo = __builtin_bit_cast(unsigned short, (bf16)f[2 * i]);
-    const unsigned short hi = __builtin_bit_cast(unsigned short, (bf16)f[2 * i + 1]);
-    u[i] = (unsigned int)lo | ((unsigned int)hi << 16);
-  }
+  for (int i = 0; i < 2; ++i) u[i] = rdn_cvt2(f[2 * i], f[2 * i + 1]);
   return u;
 }
 
@@ -128,8 +129,7 @@ __device__ __forceinline__ unsigned rdn_gate2(unsigned dy, unsigned pre, float a
       : "=&v"(m)
       : "v"(pre), "s"(0x00010001u), "s"(0x00800080u), "s"(0x000f000fu));
   const float lo = __builtin_bit_cast(float, dy << 16) * alo, hi = __builtin_bit_cast(float, dy & 0xffff0000u) * ahi;
-  const unsigned g = (unsigned)__builtin_bit_cast(unsigned short, (bf16)lo) |
-                     ((unsigned)__builtin_bit_cast(unsigned short, (bf16)hi) << 16);
+  const unsigned g = rdn_cvt2(lo, hi);
   return (g & m) | (dy & ~m);
 }
 

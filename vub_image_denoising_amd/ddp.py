@@ -37,6 +37,20 @@ import torch
 import torch.distributed as dist
 
 
+def exposure_from_stamps(samples, ticks_per_ms):
+    """Exposed all-reduce time (ms per step) from GradSync stamp triples (t_bwd,
+    t_comm, t_after) read after each replay: (t_comm - t_bwd) less the launch gap of two
+    back-to-back stamp kernels (t_after - t_comm), floored at 0 -- the time the
+    compute stream waited for the last bucket's all-reduce after its own backward.
+    Returns {per_step, mean, max, raw_mean} or None without samples."""
+    if not samples or ticks_per_ms <= 0:
+        return None
+    raw = [(b - a) / ticks_per_ms for a, b, _ in samples]
+    exp = [max(0.0, (b - a) - (c - b)) / ticks_per_ms for a, b, c in samples]
+    return {"per_step": [round(x, 4) for x in exp], "mean": round(sum(exp) / len(exp), 4),
+            "max": round(max(exp), 4), "raw_mean": round(sum(raw) / len(raw), 4)}
+
+
 def capture_safe_env() -> None:
     """Environment for RCCL collectives inside a captured hipGraph; call before
     ``init_process_group``: no NCCL event cache (every work item owns its events, so
@@ -118,6 +132,12 @@ class GradSync:
         # done) event pairs on the compute stream -- the all-reduce time the backward did
         # not hide (bench.py exposed_allreduce_ms)
         self.timing = None
+        # set to a device int64 tensor of 3 slots to stamp every finish() with the device
+        # wall clock (rdn_stamp): [0] backward done, [1] last bucket's all-reduce done, [2]
+        # right after [1] (the launch gap to subtract).  Unlike events, the stamps are
+        # kernels, so a captured train step replays them: the exposed all-reduce time of
+        # the graph path (bench.py exposed_allreduce_ms_graph, exposure_from_stamps)
+        self.stamps = None
 
     # --- engine hooks -------------------------------------------------
     def begin(self, buf=None):
@@ -171,6 +191,8 @@ class GradSync:
         if self.timing is not None and self.overlap:
             e0 = torch.cuda.Event(enable_timing=True)
             e0.record(torch.cuda.current_stream())   # the backward's last kernel is behind this
+        if self.stamps is not None and self.overlap:
+            self._stamp(0)
         for b in range(len(self.buckets)):
             if not self._launched[b] and self.overlap:
                 self._srcs[b].append(torch.cuda.current_stream())
@@ -187,6 +209,9 @@ class GradSync:
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record(torch.cuda.current_stream())
             self.timing.append((e0, e1))
+        if self.stamps is not None and self.overlap:
+            self._stamp(1)
+            self._stamp(2)
         self._works = []
         if self.world > 1:
             if self.defer_average:
@@ -202,6 +227,10 @@ class GradSync:
         torch.cuda.synchronize()
         xs = [max(0.0, a.elapsed_time(b)) for a, b in self.timing]
         return sum(xs) / len(xs)
+
+    def _stamp(self, slot):
+        from . import _hip as H
+        H.check(H.lib().rdn_stamp(self.stamps.data_ptr(), slot, H.stream_ptr()), "stamp")
 
     def take_pending(self):
         """The 1/world factor a deferred finish() left unapplied (None if none);
