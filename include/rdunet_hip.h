@@ -121,6 +121,15 @@ typedef struct rdn_conv_desc {
 
 /* Implicit-GEMM convolution (MFMA) with the fused epilogue above. */
 int rdn_conv_fwd(const rdn_conv_desc* d, void* stream);
+/* Split-K form of rdn_conv_fwd for 3x3 convs whose pixel grid is too small to fill the
+   device (a batch-1 forward's deep levels, UNet/RDUNet_model.py:157-186): the input
+   channels are walked in `splits` slices by separate blocks, each storing raw fp32 sums to
+   ws (rdn_conv_fwd_splitk_workspace_size bytes), then one launch sums the slices in slice
+   order (deterministic) and applies d's epilogue.  splits must equal rdn_conv_fwd_splits(d)
+   (0: not split -- rdn_conv_fwd); no input gate / gate-out / scatter, ncols % 4 == 0. */
+int32_t rdn_conv_fwd_splits(const rdn_conv_desc* d);
+int64_t rdn_conv_fwd_splitk_workspace_size(const rdn_conv_desc* d, int32_t splits);
+int rdn_conv_fwd_splitk(const rdn_conv_desc* d, int32_t splits, float* ws, void* stream);
 /* partial rows the gate-out epilogue of d writes (d->gout set; nothing is
    launched); 0 when the kernel rdn_conv_fwd picks for d has no gate-out form
    (launch the separate rdn_prelu_bwd instead) */

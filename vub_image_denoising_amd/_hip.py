@@ -101,6 +101,9 @@ SIGNATURES = {
     "rdn_conv_dgrad_wgrad_kernel_name": (_i32, [C.POINTER(ConvDesc), C.POINTER(WgradDesc), C.c_char_p, _i32]),
     "rdn_wgrad_chunks": (_i32, [C.POINTER(WgradDesc)]),
     "rdn_dense3_fwd": (_i32, [C.POINTER(Dense3Desc), _vp]),
+    "rdn_conv_fwd_splits": (_i32, [C.POINTER(ConvDesc)]),
+    "rdn_conv_fwd_splitk_workspace_size": (_i64, [C.POINTER(ConvDesc), _i32]),
+    "rdn_conv_fwd_splitk": (_i32, [C.POINTER(ConvDesc), _i32, _vp, _vp]),
     "rdn_dense3_kernel_name": (_i32, [C.POINTER(Dense3Desc), C.c_char_p, _i32]),
     "rdn_wgrad_workspace_size": (_i64, [C.POINTER(WgradDesc)]),
     "rdn_wgrad_reduce": (_i32, [_vp, _i32, _i32, _i32, _i32, _i32, _vp, _i32, _vp, _i32, _vp, _vp, _vp]),

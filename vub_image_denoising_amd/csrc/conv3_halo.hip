@@ -32,8 +32,12 @@ constexpr int ROWB = 160;                  // B-stage row: 128 B + 32 B pad (con
 
 // occupancy request: narrow tiles keep 2 waves/SIMD, wide tiles let the
 // register allocator use up to 512 VGPRs (measured faster: scripts/kbench.py)
-template <typename T, int BN, int WMW, int CK, bool GATE, bool PAIR_OK>
-__global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_conv_desc d, int tiles_x, int tiles_y) {
+// SPLIT (rdn_conv_fwd_splitk): block row blockIdx.y walks input-channel chunks
+// [y * c_per, (y + 1) * c_per) only and stores its raw fp32 tile to ws[y][pixel][ncols];
+// conv_splitk_reduce_kernel sums the slices in a fixed order and applies the epilogue
+template <typename T, int BN, int WMW, int CK, bool GATE, bool PAIR_OK, bool SPLIT = false>
+__global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_conv_desc d, int tiles_x, int tiles_y,
+                                                                          int c_per = 0, float* __restrict__ ws = nullptr) {
   constexpr int ES = sizeof(T);
   constexpr int VEC = TypeInfo<T>::VEC;
   constexpr int SK = 128 / ES;                       // k per stage
@@ -88,7 +92,8 @@ __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_
   const int y0 = ty * TH, x0 = tx * TW;
   const int n0 = (lb - (lb / ncb) * ncb) * BN;
   const int H = d.h, W = d.w;
-  const int nch = d.cin / CK;
+  const int c_lo = SPLIT ? (int)blockIdx.y * c_per : 0;
+  const int nch = SPLIT ? min(d.cin / CK, c_lo + c_per) : d.cin / CK;
 
   // ---- halo units of this thread (tile fixed for the block): element offset
   // from the halo origin, LDS offset, in-image flag; chunk c adds c * CK
@@ -228,13 +233,13 @@ __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_
     }
   };
 
-  load_halo(0);
-  load_b(0, 0);
+  load_halo(c_lo);
+  load_b(c_lo, 0);
   store_halo();
   store_b(0, 0);
   __syncthreads();
   int buf = 0;
-  for (int c = 0; c < nch; ++c) {
+  for (int c = c_lo; c < nch; ++c) {
     const bool more = c + 1 < nch;
     if (more) load_halo(c + 1);   // in flight during this chunk's stages
 #pragma unroll
@@ -285,6 +290,16 @@ __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_
         Ct[((wm * WTM + i * 16 + g * 4 + e) * CROW) / 4 + wn * WTN + jn * 16 + r] = acc[i][jn][e];
   __syncthreads();
 
+  if constexpr (SPLIT) {   // raw fp32 slice of the tile: 16-B units of 4 columns (ncols % 4 == 0)
+    float* const wz = ws + (int64_t)blockIdx.y * ((int64_t)d.n * H * W) * d.ncols;
+    for (int u = tid; u < BM * (BN / 4); u += NT) {
+      const int px = u / (BN / 4), cl = (u - px * (BN / 4)) * 4, c = n0 + cl;
+      const int yy = y0 + px / TW, xx = x0 + px % TW;
+      if (yy >= H || xx >= W || c >= d.ncols) continue;
+      *(f32x4*)(wz + (((int64_t)nimg * H + yy) * W + xx) * d.ncols + c) = *(const f32x4*)(Ct + (px * CROW) / 4 + cl);
+    }
+    return;
+  }
   if (!fast) {
     c3::store_tile<T, BN, NT>(d, Ct, CROW / 4, y0, x0, nimg, n0, tid);
     return;
@@ -395,10 +410,17 @@ __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_
 }
 
 template <typename T, int BN, int WMW, int CK>
-int launch_h(const rdn_conv_desc* d, hipStream_t st) {
+int launch_h(const rdn_conv_desc* d, hipStream_t st, int splits = 0, float* ws = nullptr) {
   const int tiles_x = (d->w + TW - 1) / TW, tiles_y = (d->h + TH - 1) / TH;
   const int64_t blocks = (int64_t)d->n * tiles_x * tiles_y * ((d->ncols + BN - 1) / BN);
   dim3 grid((unsigned)blocks);
+  if (splits > 0) {   // split-K slices (rdn_conv_fwd_splitk); no gate / gate-out here
+    const int nch = d->cin / CK, c_per = (nch + splits - 1) / splits;
+    RDN_PROBE("conv3_halo_kernel<%s,%d,%d,%d,split>", rdn_tname<T>(), BN, WMW, CK);
+    conv3_halo_kernel<T, BN, WMW, CK, false, false, true><<<dim3((unsigned)blocks, (nch + c_per - 1) / c_per), NT, 0, st>>>(
+        *d, tiles_x, tiles_y, c_per, ws);
+    return rdn_check_launch("rdn_conv_fwd_splitk(conv3)");
+  }
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -466,17 +488,17 @@ static int pick_bn(int ncols, int64_t tiles) {
 }
 
 template <typename T, int CK>
-int launch_bn(const rdn_conv_desc* d, hipStream_t st) {
+int launch_bn(const rdn_conv_desc* d, hipStream_t st, int splits = 0, float* ws = nullptr) {
   const int64_t tiles = (int64_t)d->n * ((d->h + c3::TH - 1) / c3::TH) * ((d->w + c3::TW - 1) / c3::TW);
   const int bn = d->bn ? d->bn : pick_bn(d->ncols, tiles);
   switch (bn) {
-    case 16: return launch_h<T, 16, 4, CK>(d, st);
-    case 32: return launch_h<T, 32, 4, CK>(d, st);
-    case 48: return launch_h<T, 48, 4, CK>(d, st);
-    case 64: return launch_h<T, 64, 2, CK>(d, st);
-    case 80: return launch_h<T, 80, 4, CK>(d, st);
-    case 96: return launch_h<T, 96, 4, CK>(d, st);
-    case 128: return launch_h<T, 128, 2, CK>(d, st);
+    case 16: return launch_h<T, 16, 4, CK>(d, st, splits, ws);
+    case 32: return launch_h<T, 32, 4, CK>(d, st, splits, ws);
+    case 48: return launch_h<T, 48, 4, CK>(d, st, splits, ws);
+    case 64: return launch_h<T, 64, 2, CK>(d, st, splits, ws);
+    case 80: return launch_h<T, 80, 4, CK>(d, st, splits, ws);
+    case 96: return launch_h<T, 96, 4, CK>(d, st, splits, ws);
+    case 128: return launch_h<T, 128, 2, CK>(d, st, splits, ws);
   }
   rdn_set_error("rdn_conv_fwd(conv3): unsupported bn=%d", bn);
   return RDN_E_ARG;
@@ -544,5 +566,46 @@ int rdn_conv3_launch(const rdn_conv_desc* d, hipStream_t st) {
     case 32: return launch_bn<float, 32>(d, st);
     case 16: return launch_bn<float, 16>(d, st);
     default: return launch_bn<float, 8>(d, st);
+  }
+}
+
+// ---- split-K slices of the 3x3 forward (round 6; rdn_conv_fwd_splitk, conv_gemm.hip,
+// owns the entry point and the reduce): slices for d on this device -- 0 (no split)
+// unless the tile grid covers under half of the CUs and there are >= 2 input-channel
+// chunks; then enough slices for ~2 blocks per CU, each of >= 1 chunk (rounded so that
+// every slice gets the same number of chunks)
+int rdn_conv3_splitk_slices(const rdn_conv_desc* d, int cus) {
+  if (d->gather != RDN_G_CONV3 || d->gate || d->gout || (d->flags & RDN_EPI_SCATTER2) || d->ncols % 4) return 0;
+  const int ck = rdn_conv3_chunk_impl(d->cin, d->dtype);
+  if (ck <= 0) return 0;
+  const int nch = d->cin / ck;
+  const int64_t tiles = (int64_t)d->n * ((d->h + c3::TH - 1) / c3::TH) * ((d->w + c3::TW - 1) / c3::TW);
+  const int bn = d->bn ? d->bn : pick_bn(d->ncols, tiles);
+  const int64_t base = tiles * ((d->ncols + bn - 1) / bn);
+  if (nch < 2 || 2 * base > cus) return 0;
+  int s = (int)((2 * (int64_t)cus + base - 1) / base);
+  if (s > nch) s = nch;
+  const int c_per = (nch + s - 1) / s;
+  return (nch + c_per - 1) / c_per;
+}
+
+// the slice launch: raw fp32 sums of slice y to ws[y][pixel][ncols]
+int rdn_conv3_splitk_launch(const rdn_conv_desc* d, int splits, float* ws, hipStream_t st) {
+  const int ck = rdn_conv3_chunk_impl(d->cin, d->dtype);
+  if (d->dtype == RDN_BF16) {
+    switch (ck) {
+      case 96: return launch_bn<bf16, 96>(d, st, splits, ws);
+      case 80: return launch_bn<bf16, 80>(d, st, splits, ws);
+      case 48: return launch_bn<bf16, 48>(d, st, splits, ws);
+      case 64: return launch_bn<bf16, 64>(d, st, splits, ws);
+      case 32: return launch_bn<bf16, 32>(d, st, splits, ws);
+      case 16: return launch_bn<bf16, 16>(d, st, splits, ws);
+      default: return launch_bn<bf16, 8>(d, st, splits, ws);
+    }
+  }
+  switch (ck) {
+    case 32: return launch_bn<float, 32>(d, st, splits, ws);
+    case 16: return launch_bn<float, 16>(d, st, splits, ws);
+    default: return launch_bn<float, 8>(d, st, splits, ws);
   }
 }

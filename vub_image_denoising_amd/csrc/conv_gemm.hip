@@ -19,6 +19,8 @@
 // (exact fp32, the mode parity is checked in).
 #include "conv3_tile.h"
 
+#include <cstdlib>
+
 namespace {
 
 constexpr int NT = 256;
@@ -30,8 +32,11 @@ template <> struct Taps<RDN_G_CONV3> { static constexpr int N = 9; };
 template <> struct Taps<RDN_G_S2> { static constexpr int N = 4; };
 template <> struct Taps<RDN_G_PIX> { static constexpr int N = 1; };
 
-template <typename T, int BM, int BN, int WMW, int GATHER>
-__global__ __launch_bounds__(NT) void conv_gemm_kernel(rdn_conv_desc d, FastDiv fd_w, FastDiv fd_hw) {
+// SPLIT (rdn_conv_fwd_splitk): block layer blockIdx.z walks K stages
+// [z * s_per, (z + 1) * s_per) only and stores its raw fp32 tile to ws[z][m][ncols]
+template <typename T, int BM, int BN, int WMW, int GATHER, bool SPLIT = false>
+__global__ __launch_bounds__(NT) void conv_gemm_kernel(rdn_conv_desc d, FastDiv fd_w, FastDiv fd_hw, int s_per = 0,
+                                                       float* __restrict__ ws = nullptr) {
   constexpr int VEC = TypeInfo<T>::VEC;
   constexpr int SK = U * VEC;
   constexpr int WNW = 4 / WMW;
@@ -80,8 +85,9 @@ __global__ __launch_bounds__(NT) void conv_gemm_kernel(rdn_conv_desc d, FastDiv 
 
   const int cin = d.cin;
   const int ktot = TAPS * cin;
-  const int nst = (ktot + SK - 1) / SK;
-  int tap = (ku * VEC) / cin, ci = (ku * VEC) - tap * cin;
+  const int s_lo = SPLIT ? (int)blockIdx.z * s_per : 0;
+  const int nst = SPLIT ? min((ktot + SK - 1) / SK, s_lo + s_per) : (ktot + SK - 1) / SK;
+  int tap = (s_lo * SK + ku * VEC) / cin, ci = (s_lo * SK + ku * VEC) - tap * cin;
 
   u32x4 ra[A_IT], rb[B_IT];
 
@@ -136,11 +142,11 @@ __global__ __launch_bounds__(NT) void conv_gemm_kernel(rdn_conv_desc d, FastDiv 
 
   const int frag_row = lane & 15, frag_k = (lane >> 4) * 16;
 
-  load_stage(0);
+  load_stage(s_lo);
   store_stage(0);
   __syncthreads();
-  for (int s = 0; s < nst; ++s) {
-    const int buf = s & 1;
+  for (int s = s_lo; s < nst; ++s) {
+    const int buf = (s - s_lo) & 1;
     if (s + 1 < nst) load_stage(s + 1);
 #pragma unroll
     for (int ks = 0; ks < U / 4; ++ks) {
@@ -189,6 +195,16 @@ __global__ __launch_bounds__(NT) void conv_gemm_kernel(rdn_conv_desc d, FastDiv 
       for (int e = 0; e < 4; ++e)
         Ct[(wm * WTM + i * 16 + (lane >> 4) * 4 + e) * CROW + wn * WTN + j * 16 + (lane & 15)] = acc[i][j][e];
   __syncthreads();
+  if constexpr (SPLIT) {   // raw fp32 slice of the tile: 16-B units of 4 columns (ncols % 4 == 0)
+    float* const wz = ws + (int64_t)blockIdx.z * M * d.ncols;
+    for (int u = tid; u < BM * (BN / 4); u += NT) {
+      const int r = u / (BN / 4), cl = (u - r * (BN / 4)) * 4;
+      const int64_t m = m0 + r;
+      if (m >= M || n0 + cl >= d.ncols) continue;
+      *(f32x4*)(wz + m * d.ncols + n0 + cl) = *(const f32x4*)(Ct + r * CROW + cl);
+    }
+    return;
+  }
   const int flags = d.flags;
   const int H = d.h, W = d.w;
   constexpr int UPR = BN / VEC;
@@ -295,10 +311,22 @@ __global__ __launch_bounds__(NT) void conv_gemm_kernel(rdn_conv_desc d, FastDiv 
 }
 
 template <typename T, int BM, int BN, int WMW>
-int launch_gather(const rdn_conv_desc* d, hipStream_t st) {
+int launch_gather(const rdn_conv_desc* d, hipStream_t st, int splits = 0, float* ws = nullptr) {
   const int64_t M = (int64_t)d->n * d->h * d->w;
   dim3 grid((unsigned)((M + BM - 1) / BM), (unsigned)((d->ncols + BN - 1) / BN));
   FastDiv fw = make_fastdiv((uint32_t)d->w), fhw = make_fastdiv((uint32_t)(d->h * d->w));
+  if (splits > 0) {   // split-K layers (rdn_conv_fwd_splitk): 2x2 / per-pixel gathers only
+    constexpr int SK = 8 * TypeInfo<T>::VEC;
+    const int taps = d->gather == RDN_G_S2 ? 4 : 1;
+    const int nst = (taps * d->cin + SK - 1) / SK, s_per = (nst + splits - 1) / splits;
+    grid.z = (unsigned)((nst + s_per - 1) / s_per);
+    RDN_PROBE("conv_gemm_kernel<%s,%d,%d,%d,%d,split>", rdn_tname<T>(), BM, BN, WMW, d->gather);
+    if (d->gather == RDN_G_S2)
+      conv_gemm_kernel<T, BM, BN, WMW, RDN_G_S2, true><<<grid, NT, 0, st>>>(*d, fw, fhw, s_per, ws);
+    else
+      conv_gemm_kernel<T, BM, BN, WMW, RDN_G_PIX, true><<<grid, NT, 0, st>>>(*d, fw, fhw, s_per, ws);
+    return rdn_check_launch("rdn_conv_fwd_splitk(gemm)");
+  }
   RDN_PROBE("conv_gemm_kernel<%s,%d,%d,%d,%d>", rdn_tname<T>(), BM, BN, WMW, d->gather);
   switch (d->gather) {
     case RDN_G_CONV3: conv_gemm_kernel<T, BM, BN, WMW, RDN_G_CONV3><<<grid, NT, 0, st>>>(*d, fw, fhw); break;
@@ -308,17 +336,19 @@ int launch_gather(const rdn_conv_desc* d, hipStream_t st) {
   return rdn_check_launch("rdn_conv_fwd");
 }
 
+static int gemm_bn(const rdn_conv_desc* d) {
+  return d->bn ? d->bn : d->ncols <= 16 ? 16 : d->ncols <= 32 ? 32 : d->ncols <= 64 ? 64 : 128;
+}
+
 template <typename T>
-int launch_typed(const rdn_conv_desc* d, hipStream_t st) {
-  int bn = d->bn;
-  if (bn == 0) bn = d->ncols <= 16 ? 16 : d->ncols <= 32 ? 32 : d->ncols <= 64 ? 64 : 128;
-  switch (bn) {
-    case 16: return launch_gather<T, 128, 16, 4>(d, st);
-    case 32: return launch_gather<T, 128, 32, 4>(d, st);
-    case 64: return launch_gather<T, 128, 64, 2>(d, st);
-    case 128: return launch_gather<T, 128, 128, 2>(d, st);
+int launch_typed(const rdn_conv_desc* d, hipStream_t st, int splits = 0, float* ws = nullptr) {
+  switch (gemm_bn(d)) {
+    case 16: return launch_gather<T, 128, 16, 4>(d, st, splits, ws);
+    case 32: return launch_gather<T, 128, 32, 4>(d, st, splits, ws);
+    case 64: return launch_gather<T, 128, 64, 2>(d, st, splits, ws);
+    case 128: return launch_gather<T, 128, 128, 2>(d, st, splits, ws);
   }
-  rdn_set_error("rdn_conv_fwd: unsupported bn=%d", bn);
+  rdn_set_error("rdn_conv_fwd: unsupported bn=%d", gemm_bn(d));
   return RDN_E_ARG;
 }
 
@@ -374,4 +404,145 @@ extern "C" int rdn_conv_fwd(const rdn_conv_desc* d, void* stream) {
   if (d->gather == RDN_G_CONV3) return rdn_conv3_launch(d, st);  // LDS-halo kernel (conv3_halo.hip)
   if (d->gate) { rdn_set_error("rdn_conv_fwd: the PReLU gate is supported for RDN_G_CONV3 only"); return RDN_E_ARG; }
   return d->dtype == RDN_BF16 ? launch_typed<bf16>(d, st) : launch_typed<float>(d, st);
+}
+
+// ---- split-K forward (round 6): the small-image convs of a batch-1 forward (config
+// 1's RDUNet(64) on 1 x 3 x 64^2: the level-2/3 grids are 256 / 64 pixels, 4-64 blocks on
+// 256 CUs; UNet/RDUNet_model.py:157-186).  The K walk is cut into slices that run as
+// separate blocks, each storing its raw fp32 tile to ws[slice][m][ncols]; one reduce
+// launch sums the slices in slice order (deterministic) and applies the conv epilogue
+// (c3::finish_unit: bias, PReLU input, PReLU, residual, accumulate, NCHW output, with
+// the depth-to-space scatter of the transposed conv).
+namespace {
+
+template <typename T>
+__global__ __launch_bounds__(256) void conv_splitk_reduce_kernel(rdn_conv_desc d, const float* __restrict__ ws,
+                                                                 int splits, FastDiv fd_w, FastDiv fd_hw) {
+  constexpr int VEC = TypeInfo<T>::VEC;
+  const int upr = (d.ncols + VEC - 1) / VEC;   // 16-B units per GEMM row
+  const int64_t M = (int64_t)d.n * d.h * d.w;
+  const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (u >= M * upr) return;
+  const int64_t m = u / upr;
+  const int col = (int)(u - m * upr) * VEC;
+  float v[VEC];
+#pragma unroll
+  for (int q = 0; q < VEC; ++q) v[q] = 0.f;
+  const float* p = ws + m * d.ncols + col;
+  const int64_t slice = M * d.ncols;
+  for (int z = 0; z < splits; ++z, p += slice) {
+    if (col + VEC <= d.ncols) {
+#pragma unroll
+      for (int q = 0; q < VEC; q += 4) {
+        const f32x4 t4 = *(const f32x4*)(p + q);
+        v[q] += t4[0]; v[q + 1] += t4[1]; v[q + 2] += t4[2]; v[q + 3] += t4[3];
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < VEC; ++q)
+        if (col + q < d.ncols) v[q] += p[q];
+    }
+  }
+  const int nimg = (int)fdiv((uint32_t)m, fd_hw);
+  const int rem = (int)m - nimg * d.h * d.w;
+  int y = (int)fdiv((uint32_t)rem, fd_w), x = rem - y * d.w, c = col;
+  int64_t opix = m;
+  if (d.flags & RDN_EPI_SCATTER2) {   // column tap * cout + c -> pixel (2y + dy, 2x + dx)
+    const int tp = col / d.cout;
+    c = col - tp * d.cout;
+    y = 2 * y + (tp >> 1);
+    x = 2 * x + (tp & 1);
+    opix = ((int64_t)nimg * (2 * d.h) + y) * (2 * d.w) + x;
+  }
+  c3::finish_unit<T>(d, v, c, opix, y, x, nimg, c3::PF_NONE, u32x4{0u, 0u, 0u, 0u});
+}
+
+// the split rule's CU count, scaled by RDN_SPLITK_OCC / 2 (A/B of the blocks-per-CU target)
+int device_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0, c = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        c <= 0)
+      c = 256;
+    const char* e = getenv("RDN_SPLITK_OCC");
+    const int occ = e ? atoi(e) : 2;
+    cus = c * (occ > 0 ? occ : 2) / 2;
+  }
+  return cus;
+}
+
+// slices of a 2x2 / per-pixel GEMM layer: as the 3x3 rule (conv3_halo.hip), over K stages
+int gemm_splitk_slices(const rdn_conv_desc* d, int cus) {
+  if (d->gather == RDN_G_CONV3 || d->gate || d->gout || d->ncols % 4) return 0;
+  const int vec = d->dtype == RDN_BF16 ? 8 : 4, sk = 8 * vec;
+  if ((d->flags & RDN_EPI_SCATTER2) && (d->cout % vec || d->cout * 4 != d->ncols)) return 0;
+  const int taps = d->gather == RDN_G_S2 ? 4 : 1;
+  const int nst = (taps * d->cin + sk - 1) / sk;
+  const int bn = gemm_bn(d);
+  const int64_t base = ((int64_t)d->n * d->h * d->w + 127) / 128 * ((d->ncols + bn - 1) / bn);
+  if (nst < 2 || 2 * base > cus) return 0;
+  int s = (int)((2 * (int64_t)cus + base - 1) / base);
+  if (s > nst) s = nst;
+  const int s_per = (nst + s - 1) / s;
+  return (nst + s_per - 1) / s_per;
+}
+
+int splitk_slices(const rdn_conv_desc* d) {
+  if (d->dtype != RDN_F32 && d->dtype != RDN_BF16) return 0;
+  return d->gather == RDN_G_CONV3 ? rdn_conv3_splitk_slices(d, device_cus()) : gemm_splitk_slices(d, device_cus());
+}
+
+}  // namespace
+
+extern "C" int32_t rdn_conv_fwd_splits(const rdn_conv_desc* d) {
+  if (!d) { rdn_set_error("rdn_conv_fwd_splits: null"); return RDN_E_ARG; }
+  return splitk_slices(d);
+}
+
+extern "C" int64_t rdn_conv_fwd_splitk_workspace_size(const rdn_conv_desc* d, int32_t splits) {
+  if (!d || splits <= 0) return RDN_E_ARG;
+  return (int64_t)splits * d->n * d->h * d->w * d->ncols * (int64_t)sizeof(float);
+}
+
+extern "C" int rdn_conv_fwd_splitk(const rdn_conv_desc* d, int32_t splits, float* ws, void* stream) {
+  if (!d || !ws || ((uintptr_t)ws & 15)) { rdn_set_error("rdn_conv_fwd_splitk: null / unaligned workspace"); return RDN_E_ARG; }
+  if (splits <= 0) return rdn_conv_fwd(d, stream);
+  if (splits != splitk_slices(d)) {
+    rdn_set_error("rdn_conv_fwd_splitk: splits %d != rdn_conv_fwd_splits %d for this descriptor", splits, splitk_slices(d));
+    return RDN_E_ARG;
+  }
+  if (!d->x || !d->wp || d->cin % 8 || ((uintptr_t)d->x & 15) || ((uintptr_t)d->wp & 15)) {
+    rdn_set_error("rdn_conv_fwd_splitk: null / unaligned operand, cin %% 8");
+    return RDN_E_ARG;
+  }
+  const int taps = d->gather == RDN_G_CONV3 ? 9 : d->gather == RDN_G_S2 ? 4 : 1;
+  if (d->gather == RDN_G_CONV3 ? d->kp < rdn_conv3_packed_k(d->cin, d->dtype) : taps * d->cin > d->kp) {
+    rdn_set_error("rdn_conv_fwd_splitk: kp=%d too small", d->kp);
+    return RDN_E_SHAPE;
+  }
+  if (d->gather == RDN_G_S2 ? (d->hin != 2 * d->h || d->win != 2 * d->w) : (d->hin != d->h || d->win != d->w)) {
+    rdn_set_error("rdn_conv_fwd_splitk: grid mismatch");
+    return RDN_E_SHAPE;
+  }
+  if ((d->flags & RDN_EPI_OUT_NCHW) ? !d->out_nchw : !d->out) { rdn_set_error("rdn_conv_fwd_splitk: null output"); return RDN_E_ARG; }
+  if (((d->flags & RDN_EPI_BIAS) && !d->bias) || ((d->flags & RDN_EPI_PRELU) && !d->alpha) ||
+      ((d->flags & RDN_EPI_STORE_PRE) && !d->pre) ||
+      ((d->flags & RDN_EPI_RESID) && !((d->flags & RDN_EPI_OUT_NCHW) ? (const void*)d->res_nchw : d->res))) {
+    rdn_set_error("rdn_conv_fwd_splitk: epilogue operand missing");
+    return RDN_E_ARG;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  int rc;
+  if (d->gather == RDN_G_CONV3) rc = rdn_conv3_splitk_launch(d, splits, ws, st);
+  else rc = d->dtype == RDN_BF16 ? launch_typed<bf16>(d, st, splits, ws) : launch_typed<float>(d, st, splits, ws);
+  if (rc) return rc;
+  const int vec = d->dtype == RDN_BF16 ? 8 : 4;
+  const int64_t units = (int64_t)d->n * d->h * d->w * ((d->ncols + vec - 1) / vec);
+  const unsigned blocks = (unsigned)((units + 255) / 256);
+  FastDiv fw = make_fastdiv((uint32_t)d->w), fhw = make_fastdiv((uint32_t)(d->h * d->w));
+  RDN_PROBE("conv_splitk_reduce_kernel<%s>", d->dtype == RDN_BF16 ? "bf16" : "f32");
+  if (d->dtype == RDN_BF16) conv_splitk_reduce_kernel<bf16><<<blocks, 256, 0, st>>>(*d, ws, splits, fw, fhw);
+  else conv_splitk_reduce_kernel<float><<<blocks, 256, 0, st>>>(*d, ws, splits, fw, fhw);
+  return rdn_check_launch("rdn_conv_fwd_splitk(reduce)");
 }

@@ -242,6 +242,9 @@ FUSE_DENSE = os.environ.get("RDN_DENSE", "1") != "0"
 # round 6: the level-1 blocks' conv_0..2 as one launch too (conv3_dense1.hip); RDN_DENSE1=0
 # keeps them on the three rdn_conv_fwd launches (A/B)
 FUSE_DENSE1 = os.environ.get("RDN_DENSE1", "1") != "0"
+# round 6: 3x3 forwards whose pixel grid covers under half of the CUs (a batch-1
+# forward's deep levels) run split-K (rdn_conv_fwd_splitk; RDN_SPLITK=0: off)
+SPLITK = os.environ.get("RDN_SPLITK", "1") != "0"
 
 
 def find_flat(params):
@@ -724,6 +727,28 @@ class UNetEngine:
                     d.res_climit = L.resid_c
             d.flags = flags
             L.fwd_desc = d
+        self._plan_splitk()
+
+    def _plan_splitk(self):
+        """Split-K slices of the forwards whose tile grid leaves most CUs idle
+        (rdn_conv_fwd_splits > 0: a batch-1 forward's level-2/3 convs, 256 / 64 pixels
+        at 64^2) and one workspace for their fp32 slices; forward-only engines (the
+        samplers, config 1's RDUNet forward)."""
+        if not SPLITK or self.train:
+            # (forward-only engines: a train step's gradients at batch 1 are sums over a
+            # few thousand pixels, so the fp32 reordering can flip a PReLU gate whose
+            # input is within noise of 0 and move a whole gradient by ~1/sqrt(pixels);
+            # the train step keeps the single-pass launches and their numerics)
+            return
+        lib = H.lib()
+        need = 0
+        for L in self.layers:
+            s = lib.rdn_conv_fwd_splits(C.byref(L.fwd_desc))
+            if s > 0:
+                L.extra["splitk"] = s
+                need = max(need, lib.rdn_conv_fwd_splitk_workspace_size(C.byref(L.fwd_desc), s))
+        if need:
+            self.ws_fwd = torch.empty(need // 4 + 4, dtype=torch.float32, device=self.device)
 
     def _plan_dense3(self):
         """Dense blocks whose conv_0..conv_2 forward runs as one rdn_dense3_fwd launch
@@ -1060,7 +1085,8 @@ class UNetEngine:
                 macs = Pout * L.cout * taps * L.cin
             fwd_bytes = es * (Pin * L.cin + Pout * L.cout * (2 if self.train else 1) +
                               (Pout * L.cout if L.resid is not None else 0))
-            info = {"fwd": ("fwd", L.name, self._kernel_key(L.fwd_desc), 2 * macs, fwd_bytes)}
+            fkey = self._kernel_key(L.fwd_desc) + (f",splitk{L.extra['splitk']}" if "splitk" in L.extra else "")
+            info = {"fwd": ("fwd", L.name, fkey, 2 * macs, fwd_bytes)}
             if "dense3" in L.extra:   # conv_0..2 in one launch: their algorithmic work summed below
                 info["dense3"] = None
             if self.train:
@@ -1141,7 +1167,13 @@ class UNetEngine:
                 continue
             d3 = L.extra.get("dense3")
             tok = tr.start(L.extra["info"]["dense3" if d3 is not None else "fwd"]) if tr is not None else None
-            rc = lib.rdn_dense3_fwd(C.byref(d3), st) if d3 is not None else fwd(C.byref(L.fwd_desc), st)
+            sk = L.extra.get("splitk")
+            if d3 is not None:
+                rc = lib.rdn_dense3_fwd(C.byref(d3), st)
+            elif sk:
+                rc = lib.rdn_conv_fwd_splitk(C.byref(L.fwd_desc), sk, self.ws_fwd.data_ptr(), st)
+            else:
+                rc = fwd(C.byref(L.fwd_desc), st)
             if tok is not None:
                 tr.stop(tok)
             if rc:
