@@ -375,10 +375,14 @@ def inference_bench(dev, base_filters=32):
     x64 = torch.rand(64, 3, 512, 512, device=dev) * 2 - 1
     g = SamplerGraph(dm, tuple(x64.shape), direct=True)
     t = timed(lambda: g(x64), 3)
-    eng = dm.unet._rdn_engines[(64, 512, 512, torch.bfloat16, False)][0]
-    flops = sum(L.extra["info"]["fwd"][3] for L in eng.layers)
+    # (forward-only batches past 2^23 pixels run in image chunks, engine.run_unet: the
+    # engines are keyed by the chunk's batch)
+    eng = next(p[0] for k, p in dm.unet._rdn_engines.items() if k[1:] == (512, 512, torch.bfloat16, False))
+    flops = sum(L.extra["info"]["fwd"][3] for L in eng.layers) * 64 / eng.B
     res["direct_sampling_512_b64_bf16"] = {"ms_per_call": round(1e3 * t, 2), "images_per_s": round(64 / t, 1),
-                                           "tflops": round(flops / t / 1e12, 1)}
+                                           "tflops": round(flops / t / 1e12, 1),
+                                           "frac_of_peak": round(flops / t / 1e12 / PEAK_BF16_TFLOPS, 4),
+                                           "engine_batch": eng.B}
     del g, x64
     dm.unet._rdn_engines.clear()
     torch.cuda.empty_cache()

@@ -160,6 +160,7 @@ __global__ __launch_bounds__(64 * NW, 2) void conv3_big_kernel(rdn_conv_desc d, 
   const int it_lo = (int)((int64_t)nitems * xcd / 8), it_hi = (int)((int64_t)nitems * (xcd + 1) / 8);
   int item = it_lo + (blockIdx.x >> 3);
 
+  const bool spre = (d.flags & RDN_EPI_STORE_PRE) != 0;   // (forward-only: no PReLU input kept)
   if constexpr (FWD) {
     for (int c = tid; c < d.ncols; c += NTB) {
       tab[c] = d.bias[c];
@@ -447,7 +448,7 @@ __global__ __launch_bounds__(64 * NW, 2) void conv3_big_kernel(rdn_conv_desc d, 
     const __amdgpu_buffer_rsrc_t ro = rdn_rsrc((const bf16*)d.out + pix0 * d.out_ps);
     const int ops = (int)d.out_ps, pps = (int)d.pre_ps;
     const bool col_ok = q.x0 + r < W;
-    const __amdgpu_buffer_rsrc_t rp = FWD ? rdn_rsrc((const bf16*)d.pre + pix0 * d.pre_ps) : ro;
+    const __amdgpu_buffer_rsrc_t rp = FWD && spre ? rdn_rsrc((const bf16*)d.pre + pix0 * d.pre_ps) : ro;
 #pragma unroll
     for (int jn = 0; jn < NTL; ++jn) {
       const int cl = q.n0 + wn * WTN + jn * 16 + 8 * (g >> 1);
@@ -488,7 +489,7 @@ __global__ __launch_bounds__(64 * NW, 2) void conv3_big_kernel(rdn_conv_desc d, 
             v[e] += b0[e];
             v[4 + e] += b1[e];
           }
-          int o = ok ? (prow * pps + cp) * 2 : RDN_OOB;
+          int o = ok && spre ? (prow * pps + cp) * 2 : RDN_OOB;
           asm volatile("" : "+v"(o));
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, Unit16<bf16>::pack(v)), rp, o, 0, 0);
 #pragma unroll
@@ -523,7 +524,7 @@ __global__ __launch_bounds__(64 * NW, 2) void conv3_big_kernel(rdn_conv_desc d, 
     const __amdgpu_buffer_rsrc_t rgo = GOK ? rdn_rsrc((const bf16*)d.gout + pix0 * d.gout_ps) : ro;
     const int ops = (int)d.out_ps, pps = (int)d.pre_ps;
     const bool col_ok = q.x0 + r < W;
-    const __amdgpu_buffer_rsrc_t rp = FWD ? rdn_rsrc((const bf16*)d.pre + pix0 * d.pre_ps) : ro;
+    const __amdgpu_buffer_rsrc_t rp = FWD && spre ? rdn_rsrc((const bf16*)d.pre + pix0 * d.pre_ps) : ro;
 #pragma unroll
     for (int jn = 0; jn < NTL; ++jn) {
       const int cl = q.n0 + wn * WTN + jn * 16 + g * 4;
@@ -544,7 +545,7 @@ __global__ __launch_bounds__(64 * NW, 2) void conv3_big_kernel(rdn_conv_desc d, 
         if constexpr (FWD) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] += bias[e];
-          int o = ok ? (prow * pps + cp) * 2 : RDN_OOB;
+          int o = ok && spre ? (prow * pps + cp) * 2 : RDN_OOB;
           asm volatile("" : "+v"(o));
           __builtin_amdgcn_raw_buffer_store_b64(rdn_pack4(v), rp, o, 0, 0);
 #pragma unroll
@@ -690,10 +691,14 @@ int cu_count() {
 }
 
 int epi_mode(const rdn_conv_desc* d) {
-  const int f = d->flags;
-  const int fwd = RDN_EPI_BIAS | RDN_EPI_PRELU | RDN_EPI_STORE_PRE;
+  // (a forward-only engine keeps no PReLU input: its pre stores go to the OOB offset,
+  // which the buffer descriptor drops -- round 6, the samplers' level-1..3 convs had
+  // fallen back to conv3_halo)
+  const int f = d->flags & ~RDN_EPI_STORE_PRE;
+  const int fwd = RDN_EPI_BIAS | RDN_EPI_PRELU;
   if (f == fwd) return EP_FWD;
   if (f == (fwd | RDN_EPI_RESID)) return EP_FWD_RES;
+  if (d->flags & RDN_EPI_STORE_PRE) return -1;
   if (f == 0) return EP_PLAIN;
   if (f == RDN_EPI_ACCUM) return EP_ACC;
   if (f == RDN_EPI_RESID) return EP_RES;

@@ -457,7 +457,8 @@ __global__ __launch_bounds__(256) void conv_splitk_reduce_kernel(rdn_conv_desc d
   c3::finish_unit<T>(d, v, c, opix, y, x, nimg, c3::PF_NONE, u32x4{0u, 0u, 0u, 0u});
 }
 
-// the split rule's CU count, scaled by RDN_SPLITK_OCC / 2 (A/B of the blocks-per-CU target)
+// the split rule's CU count (~2 blocks per CU as the target: 4 and 8 per CU measured the
+// same on config 1's graph forward, 1.22 ms, r06)
 int device_cus() {
   static int cus = 0;
   if (!cus) {
@@ -465,9 +466,7 @@ int device_cus() {
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
         c <= 0)
       c = 256;
-    const char* e = getenv("RDN_SPLITK_OCC");
-    const int occ = e ? atoi(e) : 2;
-    cus = c * (occ > 0 ? occ : 2) / 2;
+    cus = c;
   }
   return cus;
 }

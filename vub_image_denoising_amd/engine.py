@@ -245,6 +245,8 @@ FUSE_DENSE1 = os.environ.get("RDN_DENSE1", "1") != "0"
 # round 6: 3x3 forwards whose pixel grid covers under half of the CUs (a batch-1
 # forward's deep levels) run split-K (rdn_conv_fwd_splitk; RDN_SPLITK=0: off)
 SPLITK = os.environ.get("RDN_SPLITK", "1") != "0"
+# forward-only batches are run in chunks of at most this many pixels (run_unet)
+FWD_CHUNK_PIXELS = 1 << 23
 
 
 def find_flat(params):
@@ -1477,6 +1479,19 @@ def run_unet(module, x: torch.Tensor, t: torch.Tensor | None) -> torch.Tensor:
     x = _f32_input(x, type(module).__name__)
     fp = flat_params(module, x.device)
     B, Hh, Ww = x.size(0), x.size(2), x.size(3)
+    need_grad = torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in fp.params))
+    if not need_grad and B > 1 and B * Hh * Ww > FWD_CHUNK_PIXELS:
+        # a forward-only batch past 2^23 pixels (config 4: 64 x 512^2) runs as chunks of
+        # images: its channel-blocked level-0 buffers would otherwise put byte offsets
+        # past the 32-bit buffer-descriptor range of the fast conv kernels (conv3_ws /
+        # conv3_big / conv3_dense*, which then decline the launch), and the images are
+        # independent (no batch statistics), so the result is the same
+        bc = max(1, FWD_CHUNK_PIXELS // (Hh * Ww))
+        ys = []
+        for i in range(0, B, bc):
+            tc = t[i:i + bc] if (t is not None and t.dim() > 0 and t.size(0) == B) else t
+            ys.append(run_unet(module, x[i:i + bc], tc))
+        return torch.cat(ys, 0)
     return _run(module, (B, Hh, Ww), [x], t, fp,
                 lambda train, scratch: UNetEngine(module, B, Hh, Ww, module.compute_dtype, train, scratch=scratch))
 
