@@ -6,7 +6,7 @@ import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
-SOURCES = ["conv_gemm.hip", "conv3_halo.hip", "conv3_big.hip", "conv3_ws.hip", "conv3_wsd.hip", "conv3_dw.hip", "conv3_dense.hip", "conv3_dense1.hip", "conv_wgrad.hip", "wgrad3_halo.hip", "wgrad3_glds.hip", "pointwise.hip", "synth.hip", "metrics.hip"]
+SOURCES = ["conv_gemm.hip", "conv_pix.hip", "conv3_halo.hip", "conv3_big.hip", "conv3_ws.hip", "conv3_wsd.hip", "conv3_dw.hip", "conv3_dense.hip", "conv3_dense1.hip", "conv_wgrad.hip", "wgrad3_halo.hip", "wgrad3_glds.hip", "pointwise.hip", "synth.hip", "metrics.hip"]
 OUT = os.path.join(HERE, "librdunet_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wno-unused-command-line-argument"]

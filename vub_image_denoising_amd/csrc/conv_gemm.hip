@@ -354,6 +354,12 @@ int launch_typed(const rdn_conv_desc* d, hipStream_t st, int splits = 0, float* 
 
 }  // namespace
 
+// A/B switch of conv_pix.hip (RDN_PIX=0: the 2x2 shapes stay on conv_gemm_kernel)
+static const bool RDN_PIX = [] {
+  const char* e = getenv("RDN_PIX");
+  return !(e && e[0] == '0');
+}();
+
 extern "C" int rdn_conv_fwd(const rdn_conv_desc* d, void* stream) {
   if (!d || !d->x || !d->wp) { rdn_set_error("rdn_conv_fwd: null descriptor/pointer"); return RDN_E_ARG; }
   const int vec = d->dtype == RDN_BF16 ? 8 : 4;
@@ -403,6 +409,10 @@ extern "C" int rdn_conv_fwd(const rdn_conv_desc* d, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (d->gather == RDN_G_CONV3) return rdn_conv3_launch(d, st);  // LDS-halo kernel (conv3_halo.hip)
   if (d->gate) { rdn_set_error("rdn_conv_fwd: the PReLU gate is supported for RDN_G_CONV3 only"); return RDN_E_ARG; }
+  if (RDN_PIX) {   // streaming register-weight GEMM of the bf16 2x2 / per-pixel shapes (conv_pix.hip)
+    const int pix = rdn_conv_pix_launch(d, st);
+    if (pix <= 0) return pix;
+  }
   return d->dtype == RDN_BF16 ? launch_typed<bf16>(d, st) : launch_typed<float>(d, st);
 }
 

@@ -156,6 +156,7 @@ int rdn_conv3_chunk_impl(int cin, int dtype);
 int rdn_conv3_chunk_pow2(int cin, int cap);
 int rdn_dense3_l1_launch(const rdn_dense3_desc* d, hipStream_t st);
 int rdn_conv3_splitk_slices(const rdn_conv_desc* d, int cus);
+int rdn_conv_pix_launch(const rdn_conv_desc* d, hipStream_t st);
 int rdn_conv3_splitk_launch(const rdn_conv_desc* d, int splits, float* ws, hipStream_t st);
 int rdn_conv3_ws_launch(const rdn_conv_desc* d, int ck, hipStream_t st);
 int rdn_conv3_wsd_launch(const rdn_conv_desc* d, int ck, hipStream_t st);
