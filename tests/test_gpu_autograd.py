@@ -204,7 +204,11 @@ def test_block_forward_backward_vs_oracle(name, make, shapes, ref):
     for n, a, b in zip(names, g, ref_g):
         assert _rel(a, b) < 1e-4, (n, _rel(a, b))
     with torch.no_grad():                # inference engine: same output
-        assert torch.equal(blk(xg[0] if len(xg) == 1 else (xg[0], xg[1])), y.detach())
+        yi = blk(xg[0] if len(xg) == 1 else (xg[0], xg[1]))
+    # (bit-identical unless the forward-only engine runs split-K slices on a small grid,
+    # rdn_conv_fwd_splitk: then only the fp32 summation order of those convs differs)
+    split = any("splitk" in L.extra for k, pool in blk._rdn_engines.items() if not k[-1] for e in pool for L in e.layers)
+    assert torch.equal(yi, y.detach()) if not split else _rel(yi, y.detach()) < 1e-6, (split, _rel(yi, y.detach()))
 
 
 def test_blocks_compose_to_network():

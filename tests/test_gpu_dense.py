@@ -45,8 +45,12 @@ def _run(fuse, B, Hh, Ww, seed=0):
                                           (4, 128, 160, "8x32"), (4, 128, 160, "16x16"), (1, 64, 64, None),
                                           (2, 40, 48, None)])
 def test_dense3_bit_identical(B, Hh, Ww, tile, monkeypatch):
+    from vub_image_denoising_amd import engine as E
     if tile is not None:
         monkeypatch.setenv("RDN_DENSE_TILE", tile)
+    # (the fused and unfused builds must otherwise run the same kernels: no split-K
+    # slices in the forward-only engine of the small B1 grid, rdn_conv_fwd_splitk)
+    monkeypatch.setattr(E, "SPLITK", False)
     y0, yi0, g0, n0, _ = _run(False, B, Hh, Ww)
     y1, yi1, g1, n1, k1 = _run(True, B, Hh, Ww)
     assert n0 == 0 and n1 == 4, (n0, n1)

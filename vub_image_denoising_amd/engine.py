@@ -590,6 +590,7 @@ class UNetEngine:
         self.dtype = dtype
         self.code = H.dtype_code(dtype)
         self.train = train
+        self.module_training = bool(getattr(module, "training", False))
         dev = next(module.parameters()).device
         self.device = dev
         self.fp = params if params is not None else flat_params(module, dev)
@@ -736,11 +737,14 @@ class UNetEngine:
         (rdn_conv_fwd_splits > 0: a batch-1 forward's level-2/3 convs, 256 / 64 pixels
         at 64^2) and one workspace for their fp32 slices; forward-only engines (the
         samplers, config 1's RDUNet forward)."""
-        if not SPLITK or self.train:
-            # (forward-only engines: a train step's gradients at batch 1 are sums over a
-            # few thousand pixels, so the fp32 reordering can flip a PReLU gate whose
-            # input is within noise of 0 and move a whole gradient by ~1/sqrt(pixels);
-            # the train step keeps the single-pass launches and their numerics)
+        if not SPLITK or self.train or self.module_training:
+            # (forward-only engines of a module in eval mode: the samplers, inference.  A
+            # train step's gradients at batch 1 are sums over a few thousand pixels, so the
+            # fp32 reordering can flip a PReLU gate whose input is within noise of 0 and
+            # move a whole gradient by ~1/sqrt(pixels): train engines keep the single-pass
+            # launches; and a train-mode forward-only call -- the logged loss of a step whose
+            # gradient the reference discards, diffusion_RDUnet.forward_step_device -- keeps
+            # the train engine's kernels, so its loss is the train step's bit for bit)
             return
         lib = H.lib()
         need = 0
