@@ -230,7 +230,9 @@ int rdn_conv_dgrad_wgrad_kernel_name(const rdn_conv_desc* dgrad, const rdn_wgrad
    x channels 32-63 x_pl elements after 0-31, out[k] pixel stride 32, pre[k] plain
    [pixels][32], wp[k] packed by rdn_pack_weights CONV_FWD with the rdn_conv3_chunk
    K order of cin = 64 / 96 / 128: kp >= 576 / 896 / 1152); H % 16 == 0, W % 16 == 0.
-   x_c = 0 or 32: the level-0 form above. */
+   x_c = 0 or 32: the level-0 form above.
+   pre[k] may be NULL (a forward-only caller that keeps no PReLU input): nothing is
+   stored for it. */
 typedef struct rdn_dense3_desc {
   int32_t n, h, w;
   const void* x; int64_t x_pl;

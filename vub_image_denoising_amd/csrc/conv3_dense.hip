@@ -267,7 +267,7 @@ __global__ __launch_bounds__(NT, 1) void conv3_dense_kernel(rdn_dense3_desc d, i
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       o[k].o = rdn_rsrc((const bf16*)d.out[k] + pix0 * 16);
-      o[k].p = rdn_rsrc((const bf16*)d.pre[k] + pix0 * 16);
+      o[k].p = d.pre[k] ? rdn_rsrc((const bf16*)d.pre[k] + pix0 * 16) : rdn_rsrc_none(d.out[k]);   // (no PReLU input kept)
     }
     {
       f32x4 acc[G::NMT0 / NW];
@@ -337,7 +337,7 @@ int launch_dense(const rdn_dense3_desc* d, hipStream_t st) {
 extern "C" int rdn_dense3_fwd(const rdn_dense3_desc* d, void* stream) {
   if (!d || !d->x) { rdn_set_error("rdn_dense3_fwd: null descriptor"); return RDN_E_ARG; }
   for (int k = 0; k < 3; ++k)
-    if (!d->out[k] || !d->pre[k] || !d->wp[k] || !d->bias[k] || !d->alpha[k] ||
+    if (!d->out[k] || !d->wp[k] || !d->bias[k] || !d->alpha[k] ||
         ((uintptr_t)d->out[k] & 15) || ((uintptr_t)d->pre[k] & 15) || ((uintptr_t)d->wp[k] & 15) || d->kp[k] % 8) {
       rdn_set_error("rdn_dense3_fwd: conv %d: null or unaligned operand", k);
       return RDN_E_ARG;

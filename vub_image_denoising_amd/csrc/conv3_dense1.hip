@@ -328,7 +328,8 @@ __global__ __launch_bounds__(NT, 1) void conv3_dense1_kernel(rdn_dense3_desc d, 
   auto epilogue = [&](auto KC, const Tile& q) {
     constexpr int K = decltype(KC)::value;
     const int64_t pix0 = ((int64_t)q.n * H + q.y0) * W + q.x0;
-    const __amdgpu_buffer_rsrc_t rp = rdn_rsrc((const bf16*)d.pre[K] + pix0 * 32);
+    const __amdgpu_buffer_rsrc_t rp = d.pre[K] ? rdn_rsrc((const bf16*)d.pre[K] + pix0 * 32)
+                                               : rdn_rsrc_none(d.out[K]);   // (forward-only: no PReLU input kept)
     const __amdgpu_buffer_rsrc_t ro = rdn_rsrc((const bf16*)d.out[K] + pix0 * 32);
     const bool border = q.y0 == 0 || q.x0 == 0 || q.y0 + TH >= H || q.x0 + TW >= W;
     const float* const bk = bal + K * 64;

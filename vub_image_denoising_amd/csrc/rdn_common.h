@@ -97,6 +97,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rdn_rsrc(const void* base) {
   const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a), hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
   return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | lo), 0, RDN_OOB, 0x00020000);
 }
+// a descriptor of zero records: every access through it is out of range (stores dropped,
+// loads 0) -- the PReLU-input stores of a forward-only engine, which keeps none
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rdn_rsrc_none(const void* base) {
+  const uint64_t a = (uint64_t)(uintptr_t)base;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a), hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | lo), 0, 0, 0x00020000);
+}
 __device__ __forceinline__ u32x4 rdn_ld16(__amdgpu_buffer_rsrc_t rs, bool ok, int off_bytes) {
   int o = ok ? off_bytes : RDN_OOB;
   asm volatile("" : "+v"(o));   // opaque: keeps ONE load (hipcc otherwise splits it into two predicated ones)

@@ -245,6 +245,8 @@ FUSE_DENSE1 = os.environ.get("RDN_DENSE1", "1") != "0"
 # round 6: 3x3 forwards whose pixel grid covers under half of the CUs (a batch-1
 # forward's deep levels) run split-K (rdn_conv_fwd_splitk; RDN_SPLITK=0: off)
 SPLITK = os.environ.get("RDN_SPLITK", "1") != "0"
+# priority of the weight-gradient side stream (torch: negative = higher; A/B)
+SIDE_PRIO = int(os.environ.get("RDN_SIDE_PRIO", "0"))
 # forward-only batches are run in chunks of at most this many pixels (run_unet)
 FWD_CHUNK_PIXELS = 1 << 23
 
@@ -641,7 +643,8 @@ class UNetEngine:
             # SLOTS slots (layer b of the backward order uses slot b % SLOTS), each sized
             # for the largest layer that uses it; the dgrad chain waits for the side
             # stream only where it reuses a slot (default: one slot per layer, no waits)
-            self.side = torch.cuda.Stream(device=dev) if (dev.type == "cuda" and WGRAD_STREAM) else None
+            self.side = (torch.cuda.Stream(device=dev, priority=SIDE_PRIO) if (dev.type == "cuda" and WGRAD_STREAM)
+                         else None)
             if self.side is None:
                 self.slots = 1
             elif WGRAD_SLOTS > 0:
@@ -795,7 +798,7 @@ class UNetEngine:
                 ptr, _, c0, _ = self._slice(L.dst)
                 d.out[k] = ptr + 2 * (c0 // ps) * pl
                 pre = self.bufs.get(L.pre)
-                d.pre[k] = pre.data_ptr() if pre is not None else self._dense_scratch(L.pre, lvl, g)
+                d.pre[k] = pre.data_ptr() if pre is not None else None   # (forward-only: none kept)
                 packed = L.pack_fwd[8]
                 d.wp[k], d.kp[k] = packed.data_ptr(), packed.shape[1]
                 d.bias[k] = self.named[L.name + ".bias"].data_ptr()
@@ -803,15 +806,6 @@ class UNetEngine:
             L0.extra["dense3"] = d
             for L in Ls[1:]:
                 L.extra["dense3_skip"] = True
-
-    def _dense_scratch(self, name, lvl=0, g=16):
-        """PReLU-input target of a fused launch in an inference engine (no PRE_
-        buffers kept): one shared scratch plane per level, written and never read."""
-        if not hasattr(self, "_pre_scratch"):
-            self._pre_scratch = {}
-        if lvl not in self._pre_scratch:
-            self._pre_scratch[lvl] = torch.empty(self.P[lvl] * g, dtype=self.dtype, device=self.device)
-        return self._pre_scratch[lvl].data_ptr()
 
     def _build_bwd(self):
         lib = H.lib()
