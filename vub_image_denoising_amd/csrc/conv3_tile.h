@@ -101,6 +101,32 @@ template <typename T, int PCOLS, int NT>
 __device__ __forceinline__ void store_tile(const rdn_conv_desc& d, const float* Ct, int crow_f, int y0, int x0,
                                            int nimg, int c_base, int tid) {
   constexpr int VEC = TypeInfo<T>::VEC;
+  if (d.flags & RDN_EPI_OUT_NCHW) {
+    // the network's last conv (fp32 NCHW output + input residual, a few channels): one
+    // (channel, pixel) per thread, pixel fastest, so a wave's output / residual accesses
+    // are runs of consecutive x in one plane (round 6; through finish_unit a thread took
+    // a 16-byte unit of VEC channels of one pixel, nearly all of them padding, and wrote
+    // its 3 valid channels to 3 planes: 1.5 TB/s)
+    const int nc = d.ncols - c_base < PCOLS ? d.ncols - c_base : PCOLS;
+    const int flags = d.flags;
+#pragma nounroll
+    for (int u = tid; u < nc * BM; u += NT) {
+      const int cl = u / BM, p = u - cl * BM;
+      const int yy = y0 + p / TW, xx = x0 + p % TW;
+      if (yy >= d.h || xx >= d.w) continue;
+      const int c = c_base + cl;
+      float v = Ct[p * crow_f + cl];
+      if (flags & RDN_EPI_BIAS) v += d.bias[c];
+      const int64_t opix = ((int64_t)nimg * d.h + yy) * d.w + xx;
+      if (flags & RDN_EPI_STORE_PRE) ((T*)d.pre)[opix * d.pre_ps + rdn_coff(c, d.pre_ps, d.pre_pl)] = from_f32<T>(v);
+      if (flags & RDN_EPI_PRELU) v = v > 0.f ? v : d.alpha[c] * v;
+      const int64_t o = (((int64_t)nimg * d.cout + c) * d.h + yy) * d.w + xx;
+      if (flags & RDN_EPI_RESID) v += d.res_nchw[o];
+      if (flags & RDN_EPI_ACCUM) v += d.out_nchw[o];
+      d.out_nchw[o] = v;
+    }
+    return;
+  }
   constexpr int UPR = PCOLS / VEC;   // 16-B units per tile row
   constexpr int E_UNITS = BM * UPR;
 #pragma nounroll
