@@ -245,6 +245,10 @@ FUSE_DENSE1 = os.environ.get("RDN_DENSE1", "1") != "0"
 # round 6: 3x3 forwards whose pixel grid covers under half of the CUs (a batch-1
 # forward's deep levels) run split-K (rdn_conv_fwd_splitk; RDN_SPLITK=0: off)
 SPLITK = os.environ.get("RDN_SPLITK", "1") != "0"
+# round 6: the weight-gradient stream's split-K reduces of this many consecutive
+# layers in one rdn_wgrad_reduce_batch launch (each layer its own slab of a ring;
+# RDN_SIDE_BATCH=1: one reduce launch per layer, as before)
+SIDE_BATCH = max(1, min(8, int(os.environ.get("RDN_SIDE_BATCH", "4"))))
 # forward-only batches are run in chunks of at most this many pixels (run_unet)
 FWD_CHUNK_PIXELS = 1 << 23
 
@@ -952,9 +956,20 @@ class UNetEngine:
                       for i, n in enumerate(dwb)]
         self.pws = [self._shared(("pws", i), lambda n=n: torch.zeros((n // 4 + 3) // 4 * 4, **f32))
                     for i, n in enumerate(pwb)]
+        # the weight-gradient stream's layers (not fused): a ring of SIDE_BATCH slabs in
+        # backward order, so SIDE_BATCH consecutive layers' reduces can go in one launch
+        self.side_batch = SIDE_BATCH if self.side is not None else 1
+        self.ws_side = [self.ws] + [self._shared(("ws_side", i), lambda: torch.zeros(max(ws_need // 4, 4), **f32))
+                                    for i in range(1, self.side_batch)]
+        k = 0
+        for L in reversed(self.layers):
+            if not L.extra["dw"]:
+                L.extra["side_slab"] = k % self.side_batch
+                k += 1
         for L in self.layers:
             L.extra["pws"] = self.pws[L.extra["slot"]].data_ptr()
-            L.wgrad_desc.ws = self.ws_dw[L.extra["slot"]].data_ptr() if L.extra["dw"] else self.ws.data_ptr()
+            L.wgrad_desc.ws = (self.ws_dw[L.extra["slot"]].data_ptr() if L.extra["dw"]
+                               else self.ws_side[L.extra["side_slab"]].data_ptr())
             if L.extra["fused"]:
                 L.wgrad_desc.part = L.extra["pws"]
         for L in self.layers:   # the finisher's epilogue writes the gated layer's partials
@@ -1213,6 +1228,19 @@ class UNetEngine:
         tr = TRACER
         rev = list(reversed(self.layers))
         pending = []   # fused layers whose split-K reduces wait for one batched launch
+        spending = []  # weight-gradient-stream layers whose reduces wait for one batched launch
+        batch_side = side is not None and self.side_batch > 1
+
+        def flush_side():
+            if not spending:
+                return
+            jl = [j for _, j in spending]
+            H.check(lib.rdn_wgrad_reduce_batch((H.ReduceJob * len(jl))(*jl), len(jl), sst), "wgrad_reduce_batch(side)")
+            for Lp, _ in spending:
+                Lp.extra["ev_done"].record(side)
+                if sync is not None:
+                    sync.params_done(Lp.extra["pidx"], stream=side)
+            spending.clear()
 
         def flush():
             if not pending:
@@ -1230,10 +1258,12 @@ class UNetEngine:
 
         def wait_done(Lw):
             """The compute stream waits for layer Lw's weight-gradient work (its slot
-            free / an ordering edge); a still-batched fused layer is flushed first, so
-            its event is recorded in this pass before the wait."""
+            free / an ordering edge); a still-batched layer is flushed first, so its
+            event is recorded in this pass before the wait."""
             if any(Lp is Lw for Lp, _ in pending):
                 flush()
+            if any(Lp is Lw for Lp, _ in spending):
+                flush_side()
             main.wait_event(Lw.extra["ev_done"])
 
         for b, L in enumerate(rev):
@@ -1340,6 +1370,16 @@ class UNetEngine:
                         part_splits=sh if (nh > 1 and fused) else part_splits))
                 pending.append((L, jobs))
                 continue
+            if batch_side and not dw:
+                # the weight-gradient stream's reduce joins the batch of consecutive such
+                # layers (their slabs are distinct ring entries: side_slab)
+                spending.append((L, H.ReduceJob(
+                    ws=L.wgrad_desc.ws, grad=gbase + ow, part=pws, dalpha=gbase + oa, dbias=gbase + ob,
+                    splits=splits, mdim=mdim, ndim=ndim, ndim_real=ndim_real, taps=taps, gstride=ndim_real,
+                    gci0=0, accumulate=1, part_splits=part_splits)))
+                if len(spending) >= min(self.side_batch, H.REDUCE_BATCH_MAX):
+                    flush_side()
+                continue
             if cols < ndim:
                 # column halves of the fused kernel: each half's slabs hold its input
                 # channels; the dalpha/dbias partials are half 0's rows
@@ -1361,6 +1401,7 @@ class UNetEngine:
             if sync is not None:   # the stream this layer's gradients were completed on
                 sync.params_done(L.extra["pidx"], stream=None if side is None else (main if rst == st else side))
         flush()
+        flush_side()
         if side is not None:
             self.ev_end.record(side)
             main.wait_event(self.ev_end)
