@@ -104,3 +104,41 @@ def test_rdunet_t_batch1_forward_split_train_unsplit(hw):
     assert ns >= 1 and ntrain == 0
     assert _rel(ys, yu) < 1e-5
     assert all(np.isfinite(v.cpu().numpy()).all() for v in gs.values())
+
+
+def test_tickets_reset_between_calls_and_replays():
+    """The in-launch combine's tile tickets (c3::splitk_arrive) are left at zero by every
+    launch: repeated forwards of one engine, eager and graph-replayed, are bit-identical,
+    and a forward of a different input in between does not disturb them."""
+    import vub_image_denoising_amd as vm
+    from vub_image_denoising_amd import engine as E
+    assert E.SPLITK
+    torch.manual_seed(0)
+    m = vm.RDUNet(channels=3, base_filters=64).cuda().eval()
+    x = torch.randn(1, 3, 64, 64, generator=torch.Generator().manual_seed(7)).cuda()
+    x2 = torch.randn(1, 3, 64, 64, generator=torch.Generator().manual_seed(8)).cuda()
+    with torch.no_grad():
+        y0 = m(x).clone()
+        y2 = m(x2).clone()
+        ys = [m(x).clone() for _ in range(3)]
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        g = torch.cuda.CUDAGraph()
+        xs = x2.clone()
+        with torch.cuda.stream(s):
+            m(xs)
+            with torch.cuda.graph(g, stream=s):
+                yg = m(xs)
+        torch.cuda.current_stream().wait_stream(s)
+        reps = []
+        for inp in (x, x2, x):
+            xs.copy_(inp)
+            g.replay()
+            reps.append(yg.clone())
+        torch.cuda.synchronize()
+    nsplit = sum("splitk" in L.extra for pool in m._rdn_engines.values() for eng in pool for L in eng.layers)
+    assert nsplit >= 8
+    for y in ys:
+        assert torch.equal(y, y0)
+    assert not torch.equal(y2, y0)
+    assert torch.equal(reps[0], y0) and torch.equal(reps[2], y0) and torch.equal(reps[1], y2)

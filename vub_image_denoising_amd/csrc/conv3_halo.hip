@@ -64,7 +64,12 @@ __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_
   constexpr bool PAIR = PAIR_OK && ES == 2 && BN <= 96 && SPC >= 2;
   constexpr int RW = PAIR ? 288 : ROWB;              // LDS weight row of one (paired) stage
   constexpr int SS = PAIR ? (SPC + 1) / 2 : SPC;     // (paired) stages per chunk
-  constexpr int MAIN_BYTES = HALO_BYTES + 2 * BN * RW;
+  // WALL (split launches, <= 64 columns): a chunk's SPC weight stages are loaded at once
+  // and held in LDS together -- a split block walks one or a few chunks, so the per-stage
+  // load -> barrier chain of the double-buffered walk (9 dependent loads per fp32 chunk)
+  // was its whole time
+  constexpr bool WALL = SPLIT && !PAIR && BN <= 64 && HALO_BYTES + SPC * BN * RW <= 144 * 1024;
+  constexpr int MAIN_BYTES = HALO_BYTES + (WALL ? SPC : 2) * BN * RW;
   constexpr int CROW = BN * 4 + 16;                  // epilogue fp32 tile row
   constexpr int EPI_BYTES = BM * CROW;
   constexpr int LDS_BYTES = MAIN_BYTES > EPI_BYTES ? MAIN_BYTES : EPI_BYTES;   // (>= the 4 x 2 x BN gate-out partials)
@@ -233,6 +238,45 @@ __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_
     }
   };
 
+  if constexpr (WALL) {
+    u32x4 wall[SPC][B_IT];
+    auto load_all = [&](int c) {
+#pragma unroll
+      for (int j = 0; j < SPC; ++j)
+#pragma unroll
+        for (int it = 0; it < B_IT; ++it)
+          if (tid + it * NT < B_UNITS) wall[j][it] = *(const u32x4*)(wb + (int64_t)it * (NT / 8) * d.kp + c * KC + j * SK);
+    };
+    auto store_all = [&]() {
+#pragma unroll
+      for (int j = 0; j < SPC; ++j)
+#pragma unroll
+        for (int it = 0; it < B_IT; ++it)
+          if (tid + it * NT < B_UNITS)
+            *(u32x4*)(bst + j * (BN * RW) + ((tid >> 3) + it * (NT / 8)) * RW + ku * 16) = wall[j][it];
+    };
+    load_halo(c_lo);
+    load_all(c_lo);
+    store_halo();
+    store_all();
+    __syncthreads();
+    for (int c = c_lo; c < nch; ++c) {
+      const bool more = c + 1 < nch;
+      if (more) {   // the next chunk's halo and weights in flight during this one's taps
+        load_halo(c + 1);
+        load_all(c + 1);
+      }
+#pragma unroll
+      for (int j = 0; j < SPC; ++j) compute(j, bst + j * (BN * RW) + b_lane);
+      if (more) {
+        __syncthreads();
+        store_halo();
+        store_all();
+      }
+      __syncthreads();
+    }
+  }
+  if constexpr (!WALL) {
   load_halo(c_lo);
   load_b(c_lo, 0);
   store_halo();
@@ -260,6 +304,7 @@ __global__ __launch_bounds__(NT, (BN >= 64 ? 1 : 2)) void conv3_halo_kernel(rdn_
       store_halo();
       __syncthreads();
     }
+  }
   }
 
   // ---- epilogue: fp32 tile through LDS, then 16-byte NHWC units
@@ -583,7 +628,7 @@ int rdn_conv3_splitk_slices(const rdn_conv_desc* d, int cus) {
   const int bn = d->bn ? d->bn : pick_bn(d->ncols, tiles);
   const int64_t base = tiles * ((d->ncols + bn - 1) / bn);
   if (nch < 2 || 2 * base > cus) return 0;
-  int s = (int)((2 * (int64_t)cus + base - 1) / base);
+  int s = (int)((rdn_splitk_target(cus) + base - 1) / base);
   if (s > nch) s = nch;
   const int c_per = (nch + s - 1) / s;
   return (nch + c_per - 1) / c_per;

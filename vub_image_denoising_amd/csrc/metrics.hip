@@ -49,9 +49,10 @@ ColTiles col_tiles(int w) {
 // t owns input column ox0 - 3 + t.  The block walks its TY + 6 input rows once: each
 // row goes to a double-buffered LDS row of (gt, x) pairs (one barrier per row), thread
 // t < txo forms the horizontal 7-sums of the five moments (u, v, u^2, v^2, uv) of output
-// column ox0 + t, keeps the last 7 rows of them in registers and sums those
-// (no running-sum subtraction: each window mean is a fresh 49-term sum, as
-// exact as the oracle's); the next 7 rows' loads are in flight meanwhile.
+// column ox0 + t, keeps the last 7 rows of them in registers and a running window sum
+// (add the new row, subtract the one it replaces: 6 VALU per row instead of the 21 of a
+// fresh 7-row sum; fp32 over <= 70 rows, scipy's uniform_filter also slides a running
+// sum); the next 7 rows' loads are in flight meanwhile.
 // The kernel is VALU-issue bound, so the moments go as packed fp32
 // pairs -- (u, v) and (u^2, v^2) by one v_pk_add_f32 / v_pk_fma_f32 each, in the same
 // per-lane order and rounding as the scalar form -- the SSIM quotient takes one
@@ -104,6 +105,8 @@ __global__ __launch_bounds__(NT_MAX, 5) void image_metrics_kernel(const float* _
     h4[k] = 0.f;
   }
   float se = 0.f, ss = 0.f;
+  f32x2 m01 = {0.f, 0.f}, m23 = {0.f, 0.f};   // window sums of the last 7 rows' horizontal sums
+  float m4 = 0.f;
   float pa[WIN], pb[WIN];
 #pragma unroll
   for (int k = 0; k < WIN; ++k) load(k, pa[k], pb[k]);
@@ -133,17 +136,13 @@ __global__ __launch_bounds__(NT_MAX, 5) void image_metrics_kernel(const float* _
             s23 += uv * uv;
             s4 = __builtin_fmaf(uv[0], uv[1], s4);
           }
+          // running 7-row window sums: add row r, drop row r - 7 (the ring slot it replaces)
+          m01 += s01 - h01[k];
+          m23 += s23 - h23[k];
+          m4 += s4 - h4[k];
           h01[k] = s01; h23[k] = s23; h4[k] = s4;
           const int yo = y - R;                 // output row whose window just completed
           if (r >= 2 * R && ssim_x && yo >= y_lo && yo < y_hi) {
-            f32x2 m01 = {0.f, 0.f}, m23 = {0.f, 0.f};
-            float m4 = 0.f;
-#pragma unroll
-            for (int q = 0; q < WIN; ++q) {     // rows yo-3 .. yo+3 in order
-              m01 += h01[(k + 1 + q) % WIN];
-              m23 += h23[(k + 1 + q) % WIN];
-              m4 += h4[(k + 1 + q) % WIN];
-            }
             const f32x2 u = m01 * inv2;                       // (ux, uy)
             const f32x2 v = cov_norm * (m23 * inv2 - u * u);  // (vx, vy)
             const float vxy = cov_norm * (m4 * inv2[0] - u[0] * u[1]);

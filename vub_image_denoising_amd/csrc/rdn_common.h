@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/rdunet_hip.h"
 
@@ -162,6 +163,18 @@ int rdn_conv3_launch(const rdn_conv_desc* d, hipStream_t st);
 int rdn_conv3_chunk_impl(int cin, int dtype);
 int rdn_conv3_chunk_pow2(int cin, int cap);
 int rdn_dense3_l1_launch(const rdn_dense3_desc* d, hipStream_t st);
+// blocks a split-K forward launch aims for (conv3_halo.hip / conv_gemm.hip split rules):
+// RDN_SPLITK_TARGET blocks per CU (default 1: config 1's graph forward 1.08 -> 1.05 ms
+// against 2 per CU, r06; a launch of more blocks than CUs ran its split conv_3 layers
+// in ~16 us instead of ~9)
+inline int64_t rdn_splitk_target(int cus) {
+  static const int per = [] {
+    const char* e = getenv("RDN_SPLITK_TARGET");
+    const int v = e ? atoi(e) : 0;
+    return v > 0 ? v : 1;
+  }();
+  return (int64_t)per * cus;
+}
 int rdn_conv3_splitk_slices(const rdn_conv_desc* d, int cus);
 int rdn_conv_pix_launch(const rdn_conv_desc* d, hipStream_t st);
 int rdn_conv3_splitk_launch(const rdn_conv_desc* d, int splits, float* ws, hipStream_t st);
