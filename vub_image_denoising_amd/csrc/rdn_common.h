@@ -164,16 +164,15 @@ int rdn_conv3_chunk_impl(int cin, int dtype);
 int rdn_conv3_chunk_pow2(int cin, int cap);
 int rdn_dense3_l1_launch(const rdn_dense3_desc* d, hipStream_t st);
 // blocks a split-K forward launch aims for (conv3_halo.hip / conv_gemm.hip split rules):
-// RDN_SPLITK_TARGET blocks per CU (default 2.  1 ran config 1's graph forward 1.05 ms
-// against 1.08, r06 -- a launch of more blocks than CUs ran its split conv_3 layers in
-// ~16 us instead of ~9 -- but it splits the level-0 convs of batch B and 2B differently,
-// and the batched sampler's f1/f2 pair (one batch-2B call) is bit-identical to the two
-// batch-B calls only with equal slices: tests/test_gpu_network.py)
+// RDN_SPLITK_TARGET blocks per CU (default 1: config 1's graph forward 1.08 -> 1.05 ms
+// against 2, r06 -- an fp32 slice block is MFMA-bound, so a launch of more blocks than
+// CUs ran its split conv_3 layers in ~16 us instead of ~9.  Slices cut at weight-stage
+// instead of chunk granularity measured slower: 1.07 ms at 1, 1.18 at 2)
 inline int64_t rdn_splitk_target(int cus) {
   static const int per = [] {
     const char* e = getenv("RDN_SPLITK_TARGET");
     const int v = e ? atoi(e) : 0;
-    return v > 0 ? v : 2;
+    return v > 0 ? v : 1;
   }();
   return (int64_t)per * cus;
 }
