@@ -794,7 +794,7 @@ bool big_nw4() {
 bool big_fall() {
   static const bool on = [] {
     const char* e = getenv("RDN_BIG_FALL");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   return on;
 }
@@ -836,7 +836,9 @@ int big_dispatch(const rdn_conv_desc* d, hipStream_t st) {
     // the 320-column level-2 conv_3 input gradient on 64-column items (<= 6 per CU):
     // faster alone (B16 72-77 -> 67-69 us, profiles/r04_v17_big_fall_layers.txt) but
     // slower in the step beside the weight-gradient stream (1715 -> 1708 img/s,
-    // interleaved, r04_v18_big_fall_ab.txt): off, RDN_BIG_FALL=1 for A/B
+    // interleaved, r04_v18_big_fall_ab.txt); after round 6's changes faster at B16 in
+    // five of five interleaved rounds (1858 -> 1871 img/s, B32 2062 -> 2047,
+    // profiles/r06_big_fall_ab.txt): on, RDN_BIG_FALL=0 for the conv3_halo fallback
     if (!(big_fall() && d->ncols % 64 == 0 && tiles * (d->ncols / 64) <= 6ll * cus)) return 1;
   }
   if (d->ncols % 64 == 0) {
